@@ -1,0 +1,191 @@
+/*
+ * psg.h — C ABI of the MI355X batched Heard-Of (HO) round executor and
+ * Spec checker ("PSync GPU", psg).
+ *
+ * This is the drop-in boundary for ONE path of dzufferey/round (PSync): lockstep
+ * execution of closed `Round`s over many independent consensus instances under
+ * an HO schedule, with the algorithm's `Spec` evaluated after every round.
+ *
+ * What each entry point replaces in the reference (paths relative to the
+ * reference root; psync/ = src/main/scala/psync/, example/ = src/test/scala/example/):
+ *
+ *   psg_create          Algorithm construction + `Runtime.apply` backend choice
+ *                       (psync/Algorithm.scala:13-31, psync/runtime/Runtime.scala:167-177)
+ *                       and `RtProcess.setGroup` (psync/Process.scala:45-51): n, dense pids.
+ *   psg_load_inputs     the per-process `ConsensusIO.initialValue` handed to
+ *                       `Process.init(io)` (example/Otr.scala:21-26, LastVoting.scala:97-109, ...)
+ *   psg_run_batch       `Algorithm.startInstance` for a range of instances
+ *                       (psync/Algorithm.scala:36-42) followed by the whole
+ *                       `InstanceHandler.run` round loop (psync/runtime/InstanceHandler.scala:164-258):
+ *                       `init()` / `send` / `receive*` / `update` per round
+ *                       (psync/Process.scala:67-82, psync/Round.scala:57-69, 102-124),
+ *                       plus concrete evaluation of the `Spec` (psync/Specs.scala:8-16)
+ *                       that the reference only checks symbolically
+ *                       (psync/verification/Verifier.scala:111-275).
+ *   psg_fetch_instances per-instance `ConsensusIO.decide` callbacks and final
+ *                       process state for a sampled subset (the parity path).
+ *   psg_last_error      `Logger.logAndThrow` messages (InstanceHandler.scala:346,351).
+ *   psg_destroy         `Algorithm.stopInstance` / `Runtime.shutdown` (Runtime.scala:130-143).
+ *
+ * Conventions: every function returns 0 on success and a negative errno-style
+ * code on failure (no exception, no abort crosses the ABI). The caller owns all
+ * host buffers; the library owns device memory. A context is bound to one HIP
+ * device and is single-threaded. One process per GPU: multi-GPU runs shard the
+ * global instance-id range across processes (results are bit-identical for any
+ * sharding because every random draw is keyed on the global instance id).
+ */
+#ifndef PSG_H
+#define PSG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSG_ABI_VERSION 1u
+
+/* Algorithms, keyed on the reference class names. */
+enum psg_alg {
+  PSG_ALG_OTR = 1,         /* example.OTR            example/Otr.scala:13-128 */
+  PSG_ALG_LAST_VOTING = 2, /* example.LastVoting     example/LastVoting.scala:11-212 */
+  PSG_ALG_FLOODMIN = 3,    /* example.FloodMin       example/FloodMin.scala:8-48 */
+  PSG_ALG_KSET = 4,        /* example.KSetAgreement  example/KSetAgreement.scala:21-87 */
+  PSG_ALG_BENOR = 5        /* example.BenOr          example/BenOr.scala:11-124 */
+};
+
+/* Which element of a Scala immutable.Map is "first" (LastVoting maxBy ties,
+ * LastVoting.scala:132; KSet find, KSetAgreement.scala:53). */
+enum psg_tiebreak {
+  PSG_TIE_CHAMP = 0,  /* Scala 2.13: insertion order (ascending pid) for <= 4 entries,
+                         CHAMP hash-trie order for >= 5 entries (default) */
+  PSG_TIE_MIN_PID = 1 /* always the smallest pid */
+};
+
+/* Error codes (negative errno values). */
+#define PSG_OK 0
+#define PSG_EINVAL (-22)
+#define PSG_ENOMEM (-12)
+#define PSG_ENODEV (-19)
+#define PSG_EIO (-5)
+#define PSG_ERANGE (-34)
+
+#define PSG_MAX_N 256
+#define PSG_MAX_ROUNDS 250
+#define PSG_MAX_CHECKS 12
+#define PSG_NEVER 0xFFu /* "never" marker in uint8 check-point fields */
+
+/* Seeded adversarial HO schedule. All randomness is Philox4x32-10 keyed by
+ * (seed_lo, seed_hi) with counter (inst_lo, inst_hi, round, pid | stream<<16);
+ * see DESIGN.md "Schedule". Faults are HO sets (psync/Process.scala:14). */
+typedef struct psg_schedule {
+  uint32_t drop_log2;  /* 0: no benign loss; k>0: each non-self link lost w.p. 2^-k per round */
+  uint32_t good_p32;   /* P(round is "good") * 2^32: every HO(p) = one common set s */
+  int32_t good_min;    /* good-round common set satisfies |s| > good_min (<0: 2n/3, Otr.scala:96) */
+  int32_t crash_fmax;  /* <0: no crash; else f ~ U{0..crash_fmax} processes crash (permanent
+                          send omission from a crash round ~ U{0..R-1}; half the links
+                          survive in the crash round) */
+  int32_t ho_min;      /* <0: none; else if |HO(p)| <= ho_min then HO(p) := all
+                          (BenOr safetyPredicate |HO(p)| > n/2, BenOr.scala:92) */
+  uint32_t self_bit;   /* 1: p in HO(p) always (self send bypasses the network,
+                          psync/Round.scala:114-116); 0: pure HO */
+} psg_schedule;
+
+typedef struct psg_config {
+  uint32_t abi_version; /* must be PSG_ABI_VERSION */
+  int32_t alg;          /* enum psg_alg */
+  int32_t n;            /* processes per instance, 1..PSG_MAX_N */
+  int32_t rounds;       /* R rounds executed per instance, 1..PSG_MAX_ROUNDS */
+  uint64_t seed;
+  int32_t value_range;  /* synthetic init values uniform in {1..value_range} (BenOr: {false,true}) */
+  int32_t param;        /* OTR afterDecision (Otr.scala:89, default 2); FloodMin f (FloodMin.scala:27);
+                           KSet k (KSetAgreement.scala:56); LastVoting/BenOr: unused */
+  int32_t tiebreak;     /* enum psg_tiebreak */
+  int32_t device;       /* HIP device ordinal */
+  int32_t variant;      /* 0 = reference algorithm; 1 = test mutation */
+  uint64_t batch_capacity; /* max instances per psg_run_batch call (device buffers sized for it) */
+  psg_schedule sched;
+} psg_config;
+
+/* Aggregate result of one batch. All fields are sums over instances (so a
+ * cross-GPU all-reduce(sum) of the int64 array is the node-level result),
+ * except kernel_ns. */
+typedef struct psg_summary {
+  int64_t instances;
+  int64_t process_rounds;              /* checked process-rounds = n * R per instance */
+  int64_t fail_count[PSG_MAX_CHECKS];  /* instances in which check slot was false at some check point */
+  int64_t decided_processes;           /* processes whose decide callback fired */
+  int64_t digest;                      /* sum (mod 2^64) of per-instance digests */
+  int64_t term_hist[PSG_MAX_ROUNDS + 2]; /* [c] = instances whose Termination first held at
+                                            check point c (0..R); [R+1] = never */
+  int64_t kernel_ns;                   /* device time of the round kernel (HIP events) */
+} psg_summary;
+
+/* Per-instance result (24 bytes). Check point c = number of completed rounds
+ * (c = 0 is the initial state, c = R after the last round), i.e. the spec's r
+ * (psync/verification/Verifier.scala:159-168, 237-243). */
+typedef struct psg_instance_summary {
+  uint64_t digest;                    /* hash of every process's (decision, decision round,
+                                         halt round, final main variable) */
+  uint8_t first_fail[PSG_MAX_CHECKS]; /* first check point where slot was false; PSG_NEVER */
+  uint8_t term_round;                 /* first check point where all processes decided; PSG_NEVER */
+  uint8_t n_checks;
+  uint16_t n_decided;
+} psg_instance_summary;
+
+/* Per-process record (fetch path). */
+typedef struct psg_process_record {
+  int32_t decision;       /* value passed to ConsensusIO.decide (BenOr: 0/1); 0 if none */
+  int32_t decision_round; /* round k (0-based) of the first decide callback, -1 if none */
+  int32_t halt_round;     /* round k whose update called exitAtEndOfRound, -1 if never */
+  int32_t final_x;        /* final main variable (OTR/LV/FloodMin x, BenOr x, KSet pick(t)) */
+} psg_process_record;
+
+typedef struct psg_ctx psg_ctx;
+
+/* Fill *cfg with the defaults for algorithm alg at n processes. */
+int psg_config_default(psg_config* cfg, int32_t alg, int32_t n);
+
+/* Number of check slots of an algorithm and their names ("Safety", "Agreement", ...). */
+int psg_check_count(int32_t alg);
+const char* psg_check_name(int32_t alg, int32_t slot);
+
+/* Map a reference class name ("example.OTR", "example.LastVoting", ...) to an alg id. */
+int psg_alg_from_class(const char* class_name);
+
+int psg_create(psg_ctx** out, const psg_config* cfg);
+
+/* Stage the initial values of instances [inst_begin, inst_begin+inst_count) in
+ * HBM, layout [instance][pid] int32. host_init == NULL: seeded synthetic values
+ * generated on the device. A later psg_run_batch over exactly this range reads
+ * them; any other range regenerates seeded values first (outside kernel_ns). */
+int psg_load_inputs(psg_ctx* ctx, uint64_t inst_begin, uint64_t inst_count,
+                    const int32_t* host_init);
+
+/* Execute R rounds of instances [inst_begin, inst_begin+inst_count) and evaluate
+ * the Spec after every round. per_inst (nullable) receives inst_count
+ * per-instance summaries. Blocks until the results are on the host. */
+int psg_run_batch(psg_ctx* ctx, uint64_t inst_begin, uint64_t inst_count,
+                  psg_summary* out, psg_instance_summary* per_inst);
+
+/* Copy the per-process decide results of the last batch: decision [count][n]
+ * int32 and decision_round [count][n] int32 (-1 = none). Either may be NULL. */
+int psg_copy_decisions(psg_ctx* ctx, int32_t* decision, int32_t* decision_round);
+
+/* Re-execute the listed global instance ids (seeded inputs) and return their
+ * summaries (k entries) and per-process records (k * n entries, nullable). */
+int psg_fetch_instances(psg_ctx* ctx, const uint64_t* ids, size_t k,
+                        psg_instance_summary* sums, psg_process_record* procs);
+
+const char* psg_last_error(const psg_ctx* ctx);
+void psg_destroy(psg_ctx* ctx);
+
+/* Library-level error text when psg_create itself fails (ctx unavailable). */
+const char* psg_create_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PSG_H */

@@ -1,0 +1,149 @@
+"""ctypes binding of the CPU oracle (oracle/psg_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py. The product path (round_amd/) never imports it.
+"""
+import ctypes as C
+import os
+import subprocess
+
+from round_amd import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+SRC = os.path.join(HERE, "psg_oracle.cpp")
+
+SPEC_DIRECT, SPEC_INTERP, SPEC_BOTH = 0, 1, 2
+
+
+def build(force=False):
+    """Compile the oracle with g++ (recipe also in oracle/Makefile)."""
+    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= max(
+            os.path.getmtime(SRC), os.path.getmtime(os.path.join(HERE, "..", "include", "psg.h"))):
+        return LIB_PATH
+    subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.oracle_run.argtypes = [C.POINTER(abi.Config), C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64),
+                                 C.POINTER(C.c_int32), C.POINTER(abi.Summary),
+                                 C.POINTER(abi.InstanceSummary), C.POINTER(abi.ProcessRecord),
+                                 C.c_int32, C.c_int32]
+        L.oracle_run.restype = C.c_int
+        L.oracle_run_explicit.argtypes = [C.POINTER(abi.Config), C.POINTER(C.c_int32), C.POINTER(C.c_uint64),
+                                          C.POINTER(abi.InstanceSummary), C.POINTER(abi.ProcessRecord),
+                                          C.POINTER(C.c_int64), C.c_int32]
+        L.oracle_run_explicit.restype = C.c_int
+        L.oracle_last_error.restype = C.c_char_p
+        L.oracle_philox.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.oracle_java_first_boolean.argtypes = [C.c_int64]
+        L.oracle_java_first_boolean.restype = C.c_int
+        L.oracle_scala_improve.argtypes = [C.c_uint32]
+        L.oracle_scala_improve.restype = C.c_uint32
+        L.oracle_scala_map_order.argtypes = [C.POINTER(C.c_int32), C.c_int32, C.c_int32, C.POINTER(C.c_int32)]
+        L.oracle_ho_mask.argtypes = [C.POINTER(abi.Config), C.c_uint64, C.c_int32, C.c_int32]
+        L.oracle_ho_mask.restype = C.c_uint64
+        L.oracle_init_value.argtypes = [C.POINTER(abi.Config), C.c_uint64, C.c_int32]
+        L.oracle_init_value.restype = C.c_int32
+        L.oracle_crash_round.argtypes = [C.POINTER(abi.Config), C.c_uint64, C.c_int32]
+        L.oracle_crash_round.restype = C.c_int32
+        _lib = L
+    return _lib
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+def _check(rc):
+    if rc != 0:
+        raise OracleError(f"oracle rc={rc}: {lib().oracle_last_error().decode()}")
+
+
+def run(cfg, inst_begin=0, count=1, ids=None, init=None, per_instance=False, records=False,
+        threads=1, spec_mode=SPEC_DIRECT):
+    """Run instances on the CPU oracle. Returns (Summary, [InstanceSummary], [ProcessRecord])."""
+    L = lib()
+    if ids is not None:
+        count = len(ids)
+        ids_arr = (C.c_uint64 * count)(*ids)
+    else:
+        ids_arr = None
+    init_arr = None
+    if init is not None:
+        flat = [int(v) for row in init for v in row]
+        init_arr = (C.c_int32 * len(flat))(*flat)
+    summ = abi.Summary()
+    pi = (abi.InstanceSummary * count)() if per_instance else None
+    rec = (abi.ProcessRecord * (count * cfg.n))() if records else None
+    rc = L.oracle_run(C.byref(cfg), inst_begin, count, ids_arr, init_arr, C.byref(summ), pi, rec,
+                      threads, spec_mode)
+    _check(rc)
+    return summ, (list(pi) if pi is not None else None), (list(rec) if rec is not None else None)
+
+
+def run_explicit(cfg, init, ho, spec_mode=SPEC_BOTH):
+    """One instance with an explicit HO schedule ho[k][p] (bit q: p hears q), n <= 64.
+
+    Returns (InstanceSummary, [ProcessRecord], trace) with trace[c] = (x[], decided[]).
+    """
+    L = lib()
+    n, R = cfg.n, cfg.rounds
+    init_arr = (C.c_int32 * n)(*init)
+    flat = [int(ho[k][p]) for k in range(R) for p in range(n)]
+    ho_arr = (C.c_uint64 * len(flat))(*flat)
+    s = abi.InstanceSummary()
+    rec = (abi.ProcessRecord * n)()
+    tr = (C.c_int64 * ((R + 1) * 2 * n))()
+    _check(L.oracle_run_explicit(C.byref(cfg), init_arr, ho_arr, C.byref(s), rec, tr, spec_mode))
+    trace = []
+    for c in range(R + 1):
+        base = c * 2 * n
+        trace.append(([tr[base + p] for p in range(n)], [tr[base + n + p] for p in range(n)]))
+    return s, list(rec), trace
+
+
+def philox(ctr, key):
+    L = lib()
+    a = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    L.oracle_philox(a, k, o)
+    return list(o)
+
+
+def java_first_boolean(seed):
+    return bool(lib().oracle_java_first_boolean(seed))
+
+
+def scala_improve(h):
+    return lib().oracle_scala_improve(h & 0xFFFFFFFF)
+
+
+def scala_map_order(keys, tiebreak=abi.PSG_TIE_CHAMP):
+    m = len(keys)
+    a = (C.c_int32 * m)(*keys)
+    o = (C.c_int32 * m)()
+    lib().oracle_scala_map_order(a, m, tiebreak, o)
+    return list(o)
+
+
+def ho_mask(cfg, inst, k, p):
+    return lib().oracle_ho_mask(C.byref(cfg), inst, k, p)
+
+
+def init_value(cfg, inst, p):
+    return lib().oracle_init_value(C.byref(cfg), inst, p)
+
+
+def crash_round(cfg, inst, p):
+    return lib().oracle_crash_round(C.byref(cfg), inst, p)
