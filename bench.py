@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark: checked process-rounds/s of OTR n=64 with every Spec check per round.
+
+Workload (BASELINE.json configs[1]): OTR n=64, 1e7 instances x
+20 rounds per GPU, seeded HO schedules (benign loss 1/8, good rounds 1/4),
+initial values uniform in {1..V}; after every round the 3 invariants and the
+Agreement/Validity/Integrity/Irrevocability properties (+ Termination round)
+are evaluated. A step = one psg_run_batch over the GPU's instance shard with
+its initial values already resident in HBM.
+
+Multi-GPU: one process per GPU (torchrun); rank r owns global instance ids
+[r*I, (r+1)*I) (weak scaling); the per-batch int64 counters are all-reduced
+with RCCL (torch.distributed backend "nccl"). Timing: barrier +
+torch.cuda.synchronize() on both sides of exactly K steps, max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# torch first: libpsg.so then binds to the HIP runtime torch loaded (one runtime per process)
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from round_amd import abi, psync  # noqa: E402
+
+B_ALG_OTR = 24  # algorithmic bytes per process-round
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--instances", type=int, default=10_000_000, help="instances per GPU")
+    ap.add_argument("--n", type=int, default=64)
+    ap.add_argument("--rounds", type=int, default=20)
+    ap.add_argument("--V", type=int, default=64, help="value-domain size of the headline line")
+    ap.add_argument("--variants", default="2,4", help="other V values reported beside the headline")
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, target_s):
+    """Time the oracle (C++ restatement, test infrastructure) on the host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.build()
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    cal = 200 * cores
+    t0 = time.perf_counter()
+    oracle.run(cfg, 0, cal, threads=cores)
+    dt = time.perf_counter() - t0
+    count = max(cal, int(cal * target_s / max(dt, 1e-3)))
+    t0 = time.perf_counter()
+    s, _, _ = oracle.run(cfg, 0, count, threads=cores)
+    dt = time.perf_counter() - t0
+    return {
+        "value": s.process_rounds / dt,
+        "unit": "process-rounds/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{count} instances of the same workload (ids 0..{count - 1}), oracle/psg_oracle.cpp, "
+                  f"{cores} threads, {dt:.1f} s",
+    }
+
+
+def run_variant(rank, world, args, V, steps, warmup):
+    dev = int(os.environ.get("LOCAL_RANK", 0))
+    I = args.instances
+    alg = psync.OTR()
+    sched = psync.HOSchedule(drop_log2=3, good_round=0.25)
+    gr = psync.GpuRound(alg, args.n, rounds=args.rounds, seed=args.seed, schedule=sched, value_range=V,
+                        device=dev, batch_capacity=I)
+    begin = rank * I
+    gr.load_inputs(begin, I)  # inputs resident in HBM before timing
+    for _ in range(warmup):
+        gr.run(begin, I)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kns = 0
+    last = None
+    for _ in range(steps):
+        last = gr.run(begin, I)
+        kns += last.summary.kernel_ns
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    # node-level result: all-reduce (sum) the int64 counters over RCCL
+    vals = abi.summary_to_list(last.summary)
+    t = torch.tensor(vals[:-1], dtype=torch.int64, device=f"cuda:{dev}")
+    tt = torch.tensor([dt, kns / max(steps, 1) / 1e9], dtype=torch.float64, device=f"cuda:{dev}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    total = abi.summary_from_list(t.cpu().tolist() + [0])
+    dt_max, kernel_s = tt.cpu().tolist()
+    cfg = gr.cfg
+    gr.close()
+    return {"summary": total, "dt": dt_max, "kernel_s": kernel_s, "cfg": cfg}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dev = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+    head = run_variant(rank, world, args, args.V, args.steps, args.warmup)
+    variants = {}
+    for v in [int(x) for x in args.variants.split(",") if x]:
+        r = run_variant(rank, world, args, v, max(1, args.steps // 2), 1)
+        pr = r["summary"].process_rounds * max(1, args.steps // 2)
+        variants[f"V={v}"] = {"value": pr / r["dt"], "kernel_ms": r["kernel_s"] * 1e3,
+                              "violations": psync.BatchResult(psync.OTR(), args.rounds, r["summary"]).violations()}
+    if rank == 0:
+        s = head["summary"]
+        steps = args.steps
+        pr_per_step = s.process_rounds  # all ranks, one step
+        value = pr_per_step * steps / head["dt"]
+        per_launch_pr = args.instances * args.n * args.rounds  # one rank's launch
+        achieved = per_launch_pr * B_ALG_OTR / head["kernel_s"] / 1e9
+        out = {
+            "metric": "checked process-rounds/sec (node), OTR n=64 w/ invariants; % HBM peak",
+            "value": value,
+            "unit": "process-rounds/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": args.warmup,
+            "ms_per_step": head["dt"] / steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic: seeded Philox4x32-10 HO schedules and initial values",
+            "config": {
+                "workload": f"OTR n={args.n}, {args.instances} instances/GPU x {args.rounds} rounds, V={args.V}, "
+                            "drop 1/8, good-round 1/4; 3 invariants + Agreement/Validity/Integrity/"
+                            "Irrevocability + Termination evaluated after every round",
+                "alg": "example.OTR",
+                "n": args.n,
+                "rounds": args.rounds,
+                "instances_per_gpu": args.instances,
+                "value_range": args.V,
+                "parallelism": f"instance-sharded x{world} (RCCL all-reduce of counters)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": "psg::otr_kernel<1>",
+                "kernel_ms": head["kernel_s"] * 1e3,
+                "bytes_per_process_round": B_ALG_OTR,
+            },
+            "checks": {
+                "violations": psync.BatchResult(psync.OTR(), args.rounds, s).violations(),
+                "termination_hist": [s.term_hist[i] for i in range(args.rounds + 2)],
+                "decided_processes": s.decided_processes,
+            },
+            "variants": variants,
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(head["cfg"], args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,431 @@
+// psg_api.hip — C ABI of include/psg.h: context, device buffers, launches.
+//
+// Replaces, for simulation, the reference's Runtime + InstanceHandler round
+// loop (psync/runtime/Runtime.scala:60-93, psync/runtime/InstanceHandler.scala:164-258):
+// one psg_run_batch call starts every instance of a range and runs all its
+// rounds inside one kernel launch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/psg.h"
+#include "psg_device.hpp"
+#include "psg_kernels.hpp"
+
+namespace psg {
+
+// Seeded synthetic initial values (the ConsensusIO.initialValue of every process).
+__global__ void gen_init_kernel(uint64_t inst_begin, uint64_t count, int n, int alg, int V, uint64_t seed,
+                                int32_t* out) {
+  const uint64_t total = count * (uint64_t)n;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = e / (uint64_t)n;
+    const int p = (int)(e - i * (uint64_t)n);
+    const uint64_t w = rword(seed, inst_begin + i, ROUND_INIT, (uint32_t)p, 0);
+    out[e] = alg == PSG_ALG_BENOR ? (int32_t)((uint32_t)w & 1u) : 1 + (int32_t)mulhi32((uint32_t)w, (uint32_t)V);
+  }
+}
+
+hipError_t launch_gen_init(uint64_t inst_begin, uint64_t count, int n, int alg, int V, uint64_t seed, int32_t* out,
+                           hipStream_t s) {
+  const uint64_t total = count * (uint64_t)n;
+  const int grid = (int)std::min<uint64_t>((total + 255) / 256, 8192);
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(gen_init_kernel, dim3(grid), dim3(256), 0, s, inst_begin, count, n, alg, V, seed, out);
+  return hipGetLastError();
+}
+
+}  // namespace psg
+
+using namespace psg;
+
+struct psg_ctx {
+  psg_config cfg;
+  int W = 1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  uint64_t cap = 0;
+  int32_t* d_init = nullptr;
+  bool staged = false;
+  uint64_t staged_begin = 0, staged_count = 0;
+  int32_t* d_dec = nullptr;
+  uint8_t* d_dround = nullptr;
+  psg_instance_summary* d_inst = nullptr;
+  unsigned long long* d_counters = nullptr;
+  uint64_t* d_ids = nullptr;
+  psg_process_record* d_rec = nullptr;
+  uint64_t fetch_cap = 0;
+  uint64_t last_count = 0;
+  int grid_max = 0;  // resident blocks for the algorithm's kernel
+  std::string err;
+};
+
+static thread_local std::string g_create_err;
+
+static int n_checks(int alg) {
+  switch (alg) {
+    case PSG_ALG_OTR: return 8;
+    case PSG_ALG_LAST_VOTING: return 7;
+    case PSG_ALG_BENOR: return 5;
+    case PSG_ALG_FLOODMIN: return 2;
+    case PSG_ALG_KSET: return 2;
+  }
+  return 0;
+}
+
+static const char* const k_names_otr[] = {"Safety", "Invariant0", "Invariant1", "Invariant2",
+                                          "Agreement", "Validity", "Integrity", "Irrevocability"};
+static const char* const k_names_lv[] = {"Safety", "Invariant0", "Invariant1", "Agreement",
+                                         "Validity", "Integrity", "Irrevocability"};
+static const char* const k_names_benor[] = {"Safety", "Invariant0", "Agreement", "Irrevocability", "SafetyPredicate"};
+static const char* const k_names_k[] = {"KAgreement", "KValidity"};
+
+static int fail(psg_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+static int hip_fail(psg_ctx* c, hipError_t e, const char* what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  return fail(c, e == hipErrorOutOfMemory ? PSG_ENOMEM : PSG_EIO, m);
+}
+
+#define HIPCHK(ctx, call)                                  \
+  do {                                                     \
+    hipError_t e_ = (call);                                \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
+  } while (0)
+
+static hipError_t launch_alg(const psg_ctx* c, const KArgs& a, int grid) {
+  switch (c->cfg.alg) {
+    case PSG_ALG_OTR: return launch_otr(a, c->W, grid, c->stream);
+    case PSG_ALG_LAST_VOTING: return launch_lv(a, c->W, grid, c->stream);
+    case PSG_ALG_FLOODMIN: return launch_floodmin(a, c->W, grid, c->stream);
+    case PSG_ALG_KSET: return launch_kset(a, c->W, grid, c->stream);
+    case PSG_ALG_BENOR: return launch_benor(a, c->W, grid, c->stream);
+  }
+  return hipErrorInvalidValue;
+}
+
+static const void* kernel_ptr(int alg, int W) {
+  switch (alg) {
+    case PSG_ALG_OTR: return otr_kernel_ptr(W);
+    case PSG_ALG_LAST_VOTING: return lv_kernel_ptr(W);
+    case PSG_ALG_FLOODMIN: return floodmin_kernel_ptr(W);
+    case PSG_ALG_KSET: return kset_kernel_ptr(W);
+    case PSG_ALG_BENOR: return benor_kernel_ptr(W);
+  }
+  return nullptr;
+}
+
+static KArgs make_args(const psg_ctx* c) {
+  KArgs a;
+  std::memset(&a, 0, sizeof(a));
+  const psg_config& f = c->cfg;
+  a.seed = f.seed;
+  a.n = f.n;
+  a.R = f.rounds;
+  a.V = f.value_range;
+  a.param = f.param;
+  a.variant = f.variant;
+  a.tiebreak = f.tiebreak;
+  a.drop_log2 = f.sched.drop_log2;
+  a.good_p32 = f.sched.good_p32;
+  a.good_min = f.sched.good_min;
+  a.crash_fmax = f.sched.crash_fmax;
+  a.ho_min = f.sched.ho_min;
+  a.self_bit = f.sched.self_bit;
+  a.counters = c->d_counters;
+  return a;
+}
+
+static int groups_per_block(int W) { return W == 1 ? 4 : 1; }
+
+static int run_kernel(psg_ctx* c, KArgs& a, uint64_t count, psg_summary* out, bool timed) {
+  const int G = groups_per_block(c->W);
+  uint64_t want = (count + G - 1) / G;
+  int grid = (int)std::min<uint64_t>(want, (uint64_t)c->grid_max);
+  if (grid < 1) grid = 1;
+  HIPCHK(c, hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long) * NCOUNTERS, c->stream));
+  if (timed) HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  HIPCHK(c, launch_alg(c, a, grid));
+  if (timed) HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  unsigned long long host[NCOUNTERS];
+  HIPCHK(c, hipMemcpyAsync(host, c->d_counters, sizeof(host), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (out) {
+    std::memset(out, 0, sizeof(*out));
+    out->instances = (int64_t)count;
+    out->process_rounds = (int64_t)count * c->cfg.n * c->cfg.rounds;
+    for (int i = 0; i < PSG_MAX_CHECKS; ++i) out->fail_count[i] = (int64_t)host[C_FAIL + i];
+    out->decided_processes = (int64_t)host[C_DECIDED];
+    out->digest = (int64_t)host[C_DIGEST];
+    for (int i = 0; i < c->cfg.rounds + 2; ++i) out->term_hist[i] = (int64_t)host[C_HIST + i];
+    if (timed) {
+      float ms = 0.f;
+      HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+      out->kernel_ns = (int64_t)((double)ms * 1e6);
+    }
+  }
+  return PSG_OK;
+}
+
+extern "C" {
+
+int psg_config_default(psg_config* cfg, int32_t alg, int32_t n) {
+  if (!cfg) return PSG_EINVAL;
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->abi_version = PSG_ABI_VERSION;
+  cfg->alg = alg;
+  cfg->n = n;
+  cfg->rounds = 20;
+  cfg->seed = 1;
+  cfg->value_range = 4;
+  cfg->param = 0;
+  cfg->tiebreak = PSG_TIE_CHAMP;
+  cfg->batch_capacity = 1u << 20;
+  cfg->sched.drop_log2 = 3;
+  cfg->sched.good_p32 = 1u << 30;
+  cfg->sched.good_min = -1;
+  cfg->sched.crash_fmax = -1;
+  cfg->sched.ho_min = -1;
+  cfg->sched.self_bit = 1;
+  switch (alg) {
+    case PSG_ALG_OTR: cfg->param = 2; break;  // afterDecision (Otr.scala:89)
+    case PSG_ALG_LAST_VOTING:
+      cfg->value_range = (1 << 15) - 1;
+      cfg->sched.drop_log2 = 4;
+      cfg->sched.good_p32 = 0;
+      cfg->sched.crash_fmax = (n - 1) / 2;
+      break;
+    case PSG_ALG_FLOODMIN:
+      cfg->param = 2;
+      cfg->rounds = 4;
+      cfg->value_range = 1000000;
+      cfg->sched.drop_log2 = 0;
+      cfg->sched.good_p32 = 0;
+      cfg->sched.crash_fmax = 2;
+      break;
+    case PSG_ALG_KSET:
+      cfg->param = 2;
+      cfg->rounds = 16;
+      cfg->value_range = 1000000;
+      cfg->sched.drop_log2 = 0;
+      cfg->sched.good_p32 = 0;
+      cfg->sched.crash_fmax = 1;
+      break;
+    case PSG_ALG_BENOR:
+      cfg->rounds = 64;
+      cfg->value_range = 2;
+      cfg->sched.drop_log2 = 2;
+      cfg->sched.good_p32 = 0;
+      cfg->sched.ho_min = n / 2;
+      break;
+    default: return PSG_EINVAL;
+  }
+  return PSG_OK;
+}
+
+int psg_check_count(int32_t alg) { return n_checks(alg); }
+
+const char* psg_check_name(int32_t alg, int32_t slot) {
+  if (slot < 0 || slot >= n_checks(alg)) return nullptr;
+  switch (alg) {
+    case PSG_ALG_OTR: return k_names_otr[slot];
+    case PSG_ALG_LAST_VOTING: return k_names_lv[slot];
+    case PSG_ALG_BENOR: return k_names_benor[slot];
+    default: return k_names_k[slot];
+  }
+}
+
+int psg_alg_from_class(const char* name) {
+  if (!name) return PSG_EINVAL;
+  static const struct { const char* n; int id; } tab[] = {
+      {"example.OTR", PSG_ALG_OTR}, {"example.LastVoting", PSG_ALG_LAST_VOTING},
+      {"example.FloodMin", PSG_ALG_FLOODMIN}, {"example.KSetAgreement", PSG_ALG_KSET},
+      {"example.BenOr", PSG_ALG_BENOR}};
+  for (auto& t : tab)
+    if (std::strcmp(t.n, name) == 0) return t.id;
+  return PSG_EINVAL;
+}
+
+const char* psg_create_error(void) { return g_create_err.c_str(); }
+
+static int validate(const psg_config* cfg, std::string& m) {
+  if (!cfg) { m = "null config"; return PSG_EINVAL; }
+  if (cfg->abi_version != PSG_ABI_VERSION) { m = "ABI version mismatch"; return PSG_EINVAL; }
+  if (cfg->alg < PSG_ALG_OTR || cfg->alg > PSG_ALG_BENOR) { m = "unknown algorithm"; return PSG_EINVAL; }
+  if (cfg->n < 1 || cfg->n > PSG_MAX_N) { m = "n out of range 1..256"; return PSG_EINVAL; }
+  if (cfg->rounds < 1 || cfg->rounds > PSG_MAX_ROUNDS) { m = "rounds out of range 1..250"; return PSG_EINVAL; }
+  if (cfg->alg != PSG_ALG_BENOR && cfg->value_range < 1) { m = "value_range must be >= 1"; return PSG_EINVAL; }
+  if (cfg->alg == PSG_ALG_KSET && cfg->param < 1) { m = "KSetAgreement needs k >= 1"; return PSG_EINVAL; }
+  if (cfg->alg == PSG_ALG_FLOODMIN && cfg->param < 0) { m = "FloodMin needs f >= 0"; return PSG_EINVAL; }
+  if (cfg->alg == PSG_ALG_OTR && cfg->param < 1) { m = "OTR needs afterDecision >= 1"; return PSG_EINVAL; }
+  if (cfg->tiebreak != PSG_TIE_CHAMP && cfg->tiebreak != PSG_TIE_MIN_PID) { m = "bad tiebreak"; return PSG_EINVAL; }
+  if (cfg->sched.drop_log2 > 16) { m = "drop_log2 > 16"; return PSG_EINVAL; }
+  if (cfg->batch_capacity < 1) { m = "batch_capacity must be >= 1"; return PSG_EINVAL; }
+  return PSG_OK;
+}
+
+int psg_create(psg_ctx** out, const psg_config* cfg) {
+  if (!out) return PSG_EINVAL;
+  *out = nullptr;
+  std::string m;
+  int rc = validate(cfg, m);
+  if (rc) { g_create_err = m; return rc; }
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0) { g_create_err = "no HIP device"; return PSG_ENODEV; }
+  if (cfg->device < 0 || cfg->device >= ndev) { g_create_err = "device ordinal out of range"; return PSG_ENODEV; }
+  psg_ctx* c = new (std::nothrow) psg_ctx();
+  if (!c) return PSG_ENOMEM;
+  c->cfg = *cfg;
+  c->W = (cfg->n + 63) / 64;
+  c->cap = cfg->batch_capacity;
+  auto bail = [&](hipError_t err, const char* what) {
+    g_create_err = std::string(what) + ": " + hipGetErrorString(err);
+    psg_destroy(c);
+    return err == hipErrorOutOfMemory ? PSG_ENOMEM : PSG_EIO;
+  };
+#define CK(call) do { hipError_t e_ = (call); if (e_ != hipSuccess) return bail(e_, #call); } while (0)
+  CK(hipSetDevice(cfg->device));
+  CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  CK(hipEventCreate(&c->ev0));
+  CK(hipEventCreate(&c->ev1));
+  const uint64_t cells = c->cap * (uint64_t)cfg->n;
+  CK(hipMalloc(&c->d_init, sizeof(int32_t) * cells));
+  CK(hipMalloc(&c->d_dec, sizeof(int32_t) * cells));
+  CK(hipMalloc(&c->d_dround, sizeof(uint8_t) * cells));
+  CK(hipMalloc(&c->d_inst, sizeof(psg_instance_summary) * c->cap));
+  CK(hipMalloc(&c->d_counters, sizeof(unsigned long long) * NCOUNTERS));
+  const void* kp = kernel_ptr(cfg->alg, c->W);
+  int per_cu = 0;
+  const int threads = c->W == 1 ? 256 : 64 * c->W;
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, threads, 0));
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, cfg->device));
+  if (per_cu < 1) per_cu = 1;
+  c->grid_max = prop.multiProcessorCount * per_cu;
+#undef CK
+  *out = c;
+  return PSG_OK;
+}
+
+int psg_load_inputs(psg_ctx* c, uint64_t inst_begin, uint64_t count, const int32_t* host_init) {
+  if (!c) return PSG_EINVAL;
+  if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const uint64_t cells = count * (uint64_t)c->cfg.n;
+  if (host_init) {
+    HIPCHK(c, hipMemcpyAsync(c->d_init, host_init, sizeof(int32_t) * cells, hipMemcpyHostToDevice, c->stream));
+  } else {
+    HIPCHK(c, launch_gen_init(inst_begin, count, c->cfg.n, c->cfg.alg, c->cfg.value_range, c->cfg.seed, c->d_init,
+                              c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->staged = true;
+  c->staged_begin = inst_begin;
+  c->staged_count = count;
+  return PSG_OK;
+}
+
+int psg_run_batch(psg_ctx* c, uint64_t inst_begin, uint64_t count, psg_summary* out, psg_instance_summary* per_inst) {
+  if (!c) return PSG_EINVAL;
+  if (count == 0) {
+    if (out) std::memset(out, 0, sizeof(*out));
+    return PSG_OK;
+  }
+  if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (!(c->staged && c->staged_begin == inst_begin && c->staged_count == count)) {
+    int rc = psg_load_inputs(c, inst_begin, count, nullptr);
+    if (rc) return rc;
+  }
+  KArgs a = make_args(c);
+  a.inst_begin = inst_begin;
+  a.count = count;
+  a.init = c->d_init;
+  a.out_decision = c->d_dec;
+  a.out_dround = c->d_dround;
+  a.out_inst = c->d_inst;
+  int rc = run_kernel(c, a, count, out, true);
+  if (rc) return rc;
+  c->last_count = count;
+  if (per_inst) {
+    HIPCHK(c, hipMemcpy(per_inst, c->d_inst, sizeof(psg_instance_summary) * count, hipMemcpyDeviceToHost));
+  }
+  return PSG_OK;
+}
+
+int psg_copy_decisions(psg_ctx* c, int32_t* decision, int32_t* decision_round) {
+  if (!c) return PSG_EINVAL;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const uint64_t cells = c->last_count * (uint64_t)c->cfg.n;
+  if (decision) HIPCHK(c, hipMemcpy(decision, c->d_dec, sizeof(int32_t) * cells, hipMemcpyDeviceToHost));
+  if (decision_round) {
+    uint8_t* tmp = new (std::nothrow) uint8_t[cells ? cells : 1];
+    if (!tmp) return fail(c, PSG_ENOMEM, "host allocation failed");
+    hipError_t e = hipMemcpy(tmp, c->d_dround, cells, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) { delete[] tmp; return hip_fail(c, e, "hipMemcpy(dround)"); }
+    for (uint64_t k = 0; k < cells; ++k) decision_round[k] = tmp[k] == 0xFF ? -1 : (int32_t)tmp[k];
+    delete[] tmp;
+  }
+  return PSG_OK;
+}
+
+int psg_fetch_instances(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_summary* sums,
+                        psg_process_record* procs) {
+  if (!c || (!ids && k)) return PSG_EINVAL;
+  if (k == 0) return PSG_OK;
+  if (k > c->cap) return fail(c, PSG_ERANGE, "fetch count exceeds batch_capacity");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (k > c->fetch_cap) {
+    if (c->d_ids) (void)hipFree(c->d_ids);
+    if (c->d_rec) (void)hipFree(c->d_rec);
+    c->d_ids = nullptr;
+    c->d_rec = nullptr;
+    c->fetch_cap = 0;
+    HIPCHK(c, hipMalloc(&c->d_ids, sizeof(uint64_t) * k));
+    HIPCHK(c, hipMalloc(&c->d_rec, sizeof(psg_process_record) * k * (uint64_t)c->cfg.n));
+    c->fetch_cap = k;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_ids, ids, sizeof(uint64_t) * k, hipMemcpyHostToDevice, c->stream));
+  KArgs a = make_args(c);
+  a.inst_begin = 0;
+  a.count = k;
+  a.ids = c->d_ids;
+  a.init = nullptr;  // seeded inputs of each listed id
+  a.out_inst = c->d_inst;
+  a.out_rec = c->d_rec;
+  int rc = run_kernel(c, a, k, nullptr, false);
+  if (rc) return rc;
+  if (sums) HIPCHK(c, hipMemcpy(sums, c->d_inst, sizeof(psg_instance_summary) * k, hipMemcpyDeviceToHost));
+  if (procs)
+    HIPCHK(c, hipMemcpy(procs, c->d_rec, sizeof(psg_process_record) * k * (uint64_t)c->cfg.n, hipMemcpyDeviceToHost));
+  return PSG_OK;
+}
+
+const char* psg_last_error(const psg_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
+
+void psg_destroy(psg_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->cfg.device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->d_init) (void)hipFree(c->d_init);
+  if (c->d_dec) (void)hipFree(c->d_dec);
+  if (c->d_dround) (void)hipFree(c->d_dround);
+  if (c->d_inst) (void)hipFree(c->d_inst);
+  if (c->d_counters) (void)hipFree(c->d_counters);
+  if (c->d_ids) (void)hipFree(c->d_ids);
+  if (c->d_rec) (void)hipFree(c->d_rec);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+}  // extern "C"

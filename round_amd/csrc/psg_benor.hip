@@ -1,0 +1,164 @@
+// psg_benor.hip — Ben-Or randomized binary consensus on gfx950.
+//
+// Reference: example/BenOr.scala:11-84 (BenOrProcess), 266-295 (spec).
+// Payloads are one or two bits per process, so every mailbox statistic is a
+// popcount of HO(p) & alive & ballot(bit). The unseeded coin
+// `util.Random.nextBoolean` (BenOr.scala:77) is java.util.Random's first
+// nextBoolean after setSeed(Philox(seed, instance, round, pid)).
+// n = 128 runs as W = 2 waves per instance with the ballot words exchanged in LDS.
+#include "psg_device.hpp"
+#include "psg_kernels.hpp"
+
+namespace psg {
+
+// Slots: 0 Safety, 1 Invariant0 (with roundInvariants(0)(0) after R0),
+// 2 Agreement, 3 Irrevocability, 4 SafetyPredicate (|HO(p)| > n/2 on the
+// effective heard-of sets, BenOr.scala:272).
+template <int W>
+PSG_DEV void benor_check(Grp<W>& g, Checks& ck, int c, bool has_old, int n, const Mask<W>& full, bool x, bool cd,
+                         int vote, bool decided, bool decision, bool old_decided, bool old_decision, bool pred) {
+  const bool noDec = !g.any(decided || cd);
+  const int cntT = mpopc(g.ballot(x));
+  const int cntF = n - cntT;
+  bool ex = false;
+  if (cntF > n / 2) ex = ex || !g.any((decided && decision) || vote == 1);
+  if (cntT > n / 2) ex = ex || !g.any((decided && !decision) || vote == 0);
+  bool inv0 = noDec || ex;
+  if (c & 1) {  // after R0: P.forall(p => p.vote.isDefined ==> |{i : i.x == p.vote.get}| > n/2)
+    const bool bad = g.any((vote == 1 && !(cntT > n / 2)) || (vote == 0 && !(cntF > n / 2)));
+    inv0 = inv0 && !bad;
+  }
+  const Mask<W> D = g.ballot(decided);
+  const bool same = !(g.any(decided && decision) && g.any(decided && !decision));
+  const bool irrev = !has_old || !g.any(old_decided && !(decided && old_decision == decision));
+  ck.note(0, inv0, c);
+  ck.note(1, inv0, c);
+  ck.note(2, same, c);
+  ck.note(3, irrev, c);
+  ck.note(4, pred, c);
+  ck.note_term(meq(D, full), c);
+}
+
+template <int W>
+__global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
+  __shared__ BlockCounters bc;
+  __shared__ uint64_t xb[2 * W];
+  __shared__ int64_t red[2 * W];
+  counters_init(&bc);
+  __syncthreads();
+  Grp<W> g;
+  grp_setup(g, a, xb, red);
+  constexpr int G = Geometry<W>::kGroups;
+  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int n = a.n;
+  const int thr = a.variant == 1 ? n / 4 : n / 2;  // BenOr.scala:68, 71 (variant 1: mutation)
+  const Mask<W> full = mfull<W>(n);
+
+  for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
+    const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
+    Sched<W> sc;
+    sc.setup(a, inst, g.pid, g.valid);
+    int32_t x0 = 0;
+    if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_BENOR);
+    // BenOrProcess state after init(io) (BenOr.scala:13-28); vote starts as None
+    bool x = x0 != 0, cd = false, decided = false, decision = false, halted = false;
+    int vote = -1;  // Option[Boolean]: -1 None, 0 Some(false), 1 Some(true)
+    int32_t dec_val = 0, dec_round = -1, halt_round = -1;
+    Checks ck;
+    ck.reset();
+    benor_check<W>(g, ck, 0, false, n, full, x, cd, vote, decided, decision, false, false, true);
+    for (int k = 0; k < a.R; ++k) {
+      const bool old_decided = decided, old_decision = decision;
+      const Mask<W> act = g.ballot(!halted);
+      bool pred = true;
+      if (many(act)) {
+        Mask<W> goodS;
+        const bool good = sc.good_round(k, goodS);
+        Mask<W> CB = mzero<W>(), CN = mzero<W>();
+        if (sc.crash_on) {
+          CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
+          CN = g.ballot(sc.crash_round == k);
+        }
+        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+        const int size = mpopc(M);
+        pred = !g.any(!halted && size <= n / 2);
+        if ((k & 1) == 0) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
+          const Mask<W> Tm = mand(g.ballot(x), act);
+          const Mask<W> CDm = mand(g.ballot(cd), act);
+          if (!halted) {
+            if (cd) {
+              dec_val = x ? 1 : 0;
+              dec_round = k;
+              decided = true;
+              decision = x;
+              halt_round = k;
+            } else {
+              const Mask<W> MT = mand(M, Tm);
+              const int cT = mpopc(MT);
+              const int cF = size - cT;
+              const bool exT = many(mand(MT, CDm));
+              const bool exF = many(mand(mandn(M, Tm), CDm));
+              if (cT > n / 2 || exT) vote = 1;
+              else if (cF > n / 2 || exF) vote = 0;
+              else vote = -1;
+              cd = many(mand(M, CDm));
+            }
+          }
+        } else {  // R1: broadcast vote — BenOr.scala:57-79
+          const Mask<W> VT = mand(g.ballot(vote == 1), act);
+          const Mask<W> VF = mand(g.ballot(vote == 0), act);
+          if (!halted) {
+            const int t = mpopc(mand(M, VT));
+            const int f = mpopc(mand(M, VF));
+            if (t > thr) {
+              x = true;
+              cd = true;
+            } else if (f > thr) {
+              x = false;
+              cd = true;
+            } else if (t > 1) {
+              x = true;
+            } else if (f > 1) {
+              x = false;
+            } else {
+              x = sc.coin(k, g.pid);
+            }
+          }
+        }
+        if (halt_round == k) halted = true;
+      }
+      benor_check<W>(g, ck, k + 1, true, n, full, x, cd, vote, decided, decision, old_decided, old_decision, pred);
+    }
+    finish_instance<W>(g, a, i, ck, 5, dec_val, dec_round, halt_round, x ? 1 : 0, &bc);
+  }
+  __syncthreads();
+  counters_flush(&bc, a.counters, 5, a.R);
+}
+
+template <int W>
+static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(benor_kernel<W>, dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_benor(const KArgs& a, int W, int grid, hipStream_t s) {
+  switch (W) {
+    case 1: return launch_w<1>(a, grid, s);
+    case 2: return launch_w<2>(a, grid, s);
+    case 3: return launch_w<3>(a, grid, s);
+    case 4: return launch_w<4>(a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+const void* benor_kernel_ptr(int W) {
+  switch (W) {
+    case 1: return (const void*)benor_kernel<1>;
+    case 2: return (const void*)benor_kernel<2>;
+    case 3: return (const void*)benor_kernel<3>;
+    case 4: return (const void*)benor_kernel<4>;
+  }
+  return nullptr;
+}
+
+}  // namespace psg

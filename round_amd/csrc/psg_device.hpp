@@ -1,0 +1,586 @@
+// psg_device.hpp — device building blocks for the MI355X (gfx950) HO executor.
+//
+// Execution model: one wave64 executes one instance, one lane per process
+// (pid = lane) for n <= 64; for n > 64 a workgroup of W = ceil(n/64) waves
+// executes one instance and cross-wave primitives exchange 64-bit ballot words
+// through LDS. HO sets are W x 64-bit masks generated on the device from a
+// counter-based RNG and never touch HBM. Mailbox primitives are ballots,
+// popcounts and shuffles over those masks.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/psg.h"
+
+#define PSG_DEV __device__ __forceinline__
+
+namespace psg {
+
+// ---------------------------------------------------------------- kernel args
+struct KArgs {
+  uint64_t inst_begin;
+  uint64_t count;
+  const uint64_t* ids;               // nullable: explicit global instance ids
+  const int32_t* init;               // nullable: [count][n] initial values (else seeded)
+  int32_t* out_decision;             // nullable: [count][n]
+  uint8_t* out_dround;               // nullable: [count][n], 0xFF = none
+  psg_instance_summary* out_inst;    // nullable: [count]
+  psg_process_record* out_rec;       // nullable: [count][n]
+  unsigned long long* counters;      // [NCOUNTERS]
+  uint64_t seed;
+  int32_t n, R, V, param, variant, tiebreak;
+  uint32_t drop_log2, good_p32;
+  int32_t good_min, crash_fmax, ho_min;
+  uint32_t self_bit;
+};
+
+// global counter layout (uint64 each)
+enum { C_FAIL = 0, C_DECIDED = PSG_MAX_CHECKS, C_DIGEST = PSG_MAX_CHECKS + 1, C_HIST = PSG_MAX_CHECKS + 2,
+       NCOUNTERS = C_HIST + PSG_MAX_ROUNDS + 2 };
+
+constexpr uint32_t ROUND_INIT = 0xFFFFFFFFu;
+constexpr uint32_t ROUND_CRASH = 0xFFFFFFFEu;
+constexpr uint32_t PID_GLOBAL = 0xFFFFu;
+constexpr uint32_t COIN_TAG = 0x80000000u;
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct U4 { uint32_t x, y, z, w; };
+
+PSG_DEV U4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+// 64-bit word j of a stream: call s = j/2 with ctr3 = base + (s << 16).
+PSG_DEV uint64_t rword(uint64_t seed, uint64_t inst, uint32_t round, uint32_t ctr3base, uint32_t j) {
+  U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), round, ctr3base + ((j >> 1) << 16), (uint32_t)seed,
+                  (uint32_t)(seed >> 32));
+  return (j & 1u) ? ((uint64_t)o.z | ((uint64_t)o.w << 32)) : ((uint64_t)o.x | ((uint64_t)o.y << 32));
+}
+
+// Sequential reader of a word stream, computing each Philox call once.
+struct WordStream {
+  uint64_t seed, inst;
+  uint32_t round, base;
+  int32_t cur;  // call index held in lo/hi, -1 = none
+  uint64_t lo, hi;
+  PSG_DEV WordStream(uint64_t s, uint64_t i, uint32_t r, uint32_t b) : seed(s), inst(i), round(r), base(b), cur(-1), lo(0), hi(0) {}
+  PSG_DEV uint64_t word(uint32_t j) {
+    const int32_t s = (int32_t)(j >> 1);
+    if (s != cur) {
+      U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), round, base + ((uint32_t)s << 16), (uint32_t)seed,
+                      (uint32_t)(seed >> 32));
+      lo = (uint64_t)o.x | ((uint64_t)o.y << 32);
+      hi = (uint64_t)o.z | ((uint64_t)o.w << 32);
+      cur = s;
+    }
+    return (j & 1u) ? hi : lo;
+  }
+};
+
+PSG_DEV uint32_t mulhi32(uint32_t a, uint32_t b) { return __umulhi(a, b); }
+
+// java.util.Random(s).nextBoolean(): BenOr coin (example/BenOr.scala:77)
+PSG_DEV bool java_first_boolean(uint64_t s) {
+  const uint64_t mult = 0x5DEECE66DULL, mask = (1ULL << 48) - 1;
+  uint64_t seed = (s ^ mult) & mask;
+  seed = (seed * mult + 0xBULL) & mask;
+  return (seed >> 47) != 0;
+}
+
+// scala.collection.Hashing.improve on ProcessID.## (= id)
+PSG_DEV uint32_t scala_improve(uint32_t h) {
+  uint32_t x = h + ~(h << 9);
+  x ^= (x >> 14);
+  x += (x << 4);
+  x ^= (x >> 10);
+  return x;
+}
+
+// Sort key of an entry in a CHAMP trie given its payload depth (max shared
+// 5-bit hash-prefix length with any other entry of the map): level by level
+// from the root, (sub-node flag, fragment); payloads precede sub-nodes.
+PSG_DEV uint64_t champ_key(uint32_t h, int depth) {
+  uint64_t key = 0;
+#pragma unroll
+  for (int l = 0; l < 7; ++l) {
+    const uint32_t frag = (h >> (5 * l)) & 31u;
+    const uint64_t unit = l < depth ? (32u | frag) : (l == depth ? frag : 0u);
+    key = (key << 6) | unit;
+  }
+  return key;
+}
+
+PSG_DEV int champ_cpl(uint32_t a, uint32_t b) {  // shared leading fragments, a != b
+  int t = __builtin_ctz(a ^ b);
+  return t / 5;
+}
+
+// ---------------------------------------------------------------- digest
+PSG_DEV uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+PSG_DEV uint64_t proc_digest(int pid, int32_t dec, int32_t dround, int32_t hround, int32_t mainx) {
+  uint64_t y = ((uint64_t)(uint32_t)pid << 32) | ((uint64_t)((uint32_t)dround & 0xFFFFu) << 16) |
+               (uint64_t)((uint32_t)hround & 0xFFFFu);
+  uint64_t z = ((uint64_t)(uint32_t)dec << 32) | (uint64_t)(uint32_t)mainx;
+  return splitmix64(z ^ splitmix64(y));
+}
+
+// ---------------------------------------------------------------- masks
+template <int W>
+struct Mask {
+  uint64_t w[W];
+};
+
+template <int W>
+PSG_DEV Mask<W> mzero() {
+  Mask<W> m;
+#pragma unroll
+  for (int i = 0; i < W; ++i) m.w[i] = 0;
+  return m;
+}
+template <int W>
+PSG_DEV Mask<W> mand(const Mask<W>& a, const Mask<W>& b) {
+  Mask<W> m;
+#pragma unroll
+  for (int i = 0; i < W; ++i) m.w[i] = a.w[i] & b.w[i];
+  return m;
+}
+template <int W>
+PSG_DEV Mask<W> mandn(const Mask<W>& a, const Mask<W>& b) {  // a & ~b
+  Mask<W> m;
+#pragma unroll
+  for (int i = 0; i < W; ++i) m.w[i] = a.w[i] & ~b.w[i];
+  return m;
+}
+template <int W>
+PSG_DEV Mask<W> mor(const Mask<W>& a, const Mask<W>& b) {
+  Mask<W> m;
+#pragma unroll
+  for (int i = 0; i < W; ++i) m.w[i] = a.w[i] | b.w[i];
+  return m;
+}
+template <int W>
+PSG_DEV int mpopc(const Mask<W>& a) {
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < W; ++i) c += __popcll(a.w[i]);
+  return c;
+}
+template <int W>
+PSG_DEV bool many(const Mask<W>& a) {
+  uint64_t o = 0;
+#pragma unroll
+  for (int i = 0; i < W; ++i) o |= a.w[i];
+  return o != 0;
+}
+template <int W>
+PSG_DEV bool meq(const Mask<W>& a, const Mask<W>& b) {
+  uint64_t o = 0;
+#pragma unroll
+  for (int i = 0; i < W; ++i) o |= a.w[i] ^ b.w[i];
+  return o == 0;
+}
+template <int W>
+PSG_DEV bool mtest(const Mask<W>& a, int q) {
+  uint64_t word = a.w[0];
+#pragma unroll
+  for (int i = 1; i < W; ++i)
+    if ((q >> 6) == i) word = a.w[i];
+  return (word >> (q & 63)) & 1ull;
+}
+template <int W>
+PSG_DEV void mset(Mask<W>& a, int q) {
+#pragma unroll
+  for (int i = 0; i < W; ++i)
+    if ((q >> 6) == i) a.w[i] |= 1ull << (q & 63);
+}
+template <int W>
+PSG_DEV void mclear(Mask<W>& a, int q) {
+#pragma unroll
+  for (int i = 0; i < W; ++i)
+    if ((q >> 6) == i) a.w[i] &= ~(1ull << (q & 63));
+}
+// first set pid (-1 if empty)
+template <int W>
+PSG_DEV int mfirst(const Mask<W>& a) {
+#pragma unroll
+  for (int i = 0; i < W; ++i)
+    if (a.w[i]) return i * 64 + __builtin_ctzll(a.w[i]);
+  return -1;
+}
+template <int W>
+PSG_DEV Mask<W> mfull(int n) {
+  Mask<W> m;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const int lo = i * 64;
+    m.w[i] = n >= lo + 64 ? ~0ull : (n <= lo ? 0ull : ((1ull << (n - lo)) - 1ull));
+  }
+  return m;
+}
+
+PSG_DEV uint64_t rfl64(uint64_t v) {
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+PSG_DEV int32_t rfl32(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+PSG_DEV int32_t readlane32(int32_t v, int q) { return __builtin_amdgcn_readlane(v, q); }
+PSG_DEV uint64_t readlane64(uint64_t v, int q) {
+  uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, q);
+  uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), q);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// ---------------------------------------------------------------- group of W waves = one instance
+// LDS per group (W > 1): ballot ping-pong [2][W] + reduction scratch [W] + staged
+// per-process arrays. For W == 1 everything stays in registers (readlane).
+template <int W>
+struct Grp {
+  int lane;   // 0..63
+  int wv;     // wave index inside the instance
+  int pid;    // wv * 64 + lane
+  bool valid; // pid < n
+  int ph;
+  uint64_t* xb;  // LDS: [2][W] ballot words
+  int64_t* red;  // LDS: [2][W] reduction words
+
+  PSG_DEV void sync() const {
+    if constexpr (W > 1) __syncthreads();
+  }
+
+  // Mask of the processes for which pred holds (pred is ANDed with valid).
+  PSG_DEV Mask<W> ballot(bool pred) {
+    const uint64_t b = __ballot(pred && valid);
+    Mask<W> m;
+    if constexpr (W == 1) {
+      m.w[0] = b;
+    } else {
+      uint64_t* s = xb + ph * W;
+      ph ^= 1;
+      if (lane == 0) s[wv] = b;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < W; ++i) m.w[i] = rfl64(s[i]);
+    }
+    return m;
+  }
+  PSG_DEV bool any(bool pred) { return many(ballot(pred)); }
+
+  // value of process q (uniform q): W==1 readlane of `mine`; W>1 from a staged LDS array.
+  PSG_DEV int32_t bcast(int32_t mine, const int32_t* staged, int q) const {
+    if constexpr (W == 1) return readlane32(mine, q);
+    else return rfl32(staged[q]);
+  }
+
+  // group reductions over valid lanes (inactive lanes contribute the identity)
+  PSG_DEV int64_t wave_min64(int64_t v) const {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      int64_t t = __shfl_xor(v, o);
+      v = t < v ? t : v;
+    }
+    return v;
+  }
+  PSG_DEV int64_t wave_max64(int64_t v) const {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      int64_t t = __shfl_xor(v, o);
+      v = t > v ? t : v;
+    }
+    return v;
+  }
+  PSG_DEV uint64_t wave_sum64(uint64_t v) const {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+  }
+  PSG_DEV int32_t wave_min32(int32_t v) const {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+  }
+  PSG_DEV int32_t wave_max32(int32_t v) const {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+  }
+  template <int OP>  // 0 min, 1 max, 2 sum
+  PSG_DEV int64_t cross64(int64_t v) {
+    if constexpr (W == 1) {
+      return v;
+    } else {
+      int64_t* s = red + ph * W;
+      ph ^= 1;
+      if (lane == 0) s[wv] = v;
+      __syncthreads();
+      int64_t r = s[0];
+#pragma unroll
+      for (int i = 1; i < W; ++i) {
+        int64_t t = s[i];
+        if (OP == 0) r = t < r ? t : r;
+        else if (OP == 1) r = t > r ? t : r;
+        else r = (int64_t)((uint64_t)r + (uint64_t)t);
+      }
+      return r;
+    }
+  }
+  PSG_DEV int64_t min64(int64_t v, bool in) { return cross64<0>(wave_min64((in && valid) ? v : INT64_MAX)); }
+  PSG_DEV int64_t max64(int64_t v, bool in) { return cross64<1>(wave_max64((in && valid) ? v : INT64_MIN)); }
+  PSG_DEV uint64_t sum64(uint64_t v) { return (uint64_t)cross64<2>((int64_t)wave_sum64(valid ? v : 0)); }
+  PSG_DEV int32_t min32(int32_t v, bool in) {
+    int32_t m = wave_min32((in && valid) ? v : INT32_MAX);
+    if constexpr (W == 1) return m;
+    else return (int32_t)cross64<0>(m);
+  }
+  PSG_DEV int32_t max32(int32_t v, bool in) {
+    int32_t m = wave_max32((in && valid) ? v : INT32_MIN);
+    if constexpr (W == 1) return m;
+    else return (int32_t)cross64<1>(m);
+  }
+};
+
+// ---------------------------------------------------------------- schedule
+template <int W>
+struct Sched {
+  uint64_t seed, inst;
+  Mask<W> full;
+  int32_t crash_round;  // this process's crash round, -1 = correct
+  bool crash_on;
+  int good_min, ho_min, V;
+  uint32_t drop, good_p32, self_bit;
+
+  PSG_DEV void setup(const KArgs& args, uint64_t i, int pid, bool valid) {
+    seed = args.seed;
+    inst = i;
+    V = args.V;
+    drop = args.drop_log2;
+    good_p32 = args.good_p32;
+    self_bit = args.self_bit;
+    ho_min = args.ho_min;
+    full = mfull<W>(args.n);
+    crash_on = args.crash_fmax >= 0;
+    good_min = args.good_min >= 0 ? args.good_min : (2 * args.n) / 3;
+    crash_round = -1;
+    if (crash_on && valid) {
+      const uint64_t w0 = rword(seed, i, ROUND_CRASH, PID_GLOBAL, 0);
+      const uint64_t w1 = rword(seed, i, ROUND_CRASH, PID_GLOBAL, 1);
+      const uint32_t f = mulhi32((uint32_t)w0, (uint32_t)args.crash_fmax + 1u);
+      const uint32_t am = (uint32_t)(w0 >> 32) | 1u;
+      const uint32_t off = (uint32_t)w1;
+      const uint32_t n = (uint32_t)args.n;
+      const bool pow2 = (n & (n - 1)) == 0;
+      const uint32_t pos = pow2 ? ((am * (uint32_t)pid + off) & (n - 1)) : (((uint32_t)pid + off % n) % n);
+      if (pos < f)
+        crash_round = (int32_t)mulhi32((uint32_t)rword(seed, i, ROUND_CRASH, (uint32_t)pid, 0), (uint32_t)args.R);
+    }
+  }
+
+  PSG_DEV int32_t init_value(int pid, int alg) const {
+    const uint64_t w = rword(seed, inst, ROUND_INIT, (uint32_t)pid, 0);
+    if (alg == PSG_ALG_BENOR) return (int32_t)((uint32_t)w & 1u);
+    return 1 + (int32_t)mulhi32((uint32_t)w, (uint32_t)V);
+  }
+
+  PSG_DEV bool coin(int k, int pid) const {
+    return java_first_boolean(rword(seed, inst, (uint32_t)k, COIN_TAG | (uint32_t)pid, 0));
+  }
+
+  // Uniform per (instance, round): good-round flag and its common HO set.
+  PSG_DEV bool good_round(int k, Mask<W>& s) const {
+    WordStream ws(seed, inst, (uint32_t)k, PID_GLOBAL);
+    const bool good = (uint32_t)ws.word(0) < good_p32;
+    s = full;
+    if (good && drop > 0) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        uint64_t m = ~0ull;
+        for (uint32_t i = 0; i < drop; ++i) m &= ws.word(1u + (uint32_t)w * drop + i);
+        s.w[w] &= ~m;
+      }
+      if (mpopc(s) <= good_min) s = full;
+    }
+    return good;
+  }
+
+  // HO(p) for this lane's process p in round k. CB = processes crashed before
+  // round k, CN = crashing in round k (uniform).
+  PSG_DEV Mask<W> ho(int k, int pid, bool good, const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CN) const {
+    WordStream ws(seed, inst, (uint32_t)k, (uint32_t)pid);
+    Mask<W> base;
+    if (good) {
+      base = goodS;
+    } else {
+      base = full;
+      if (drop > 0) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          uint64_t m = ~0ull;
+          for (uint32_t i = 0; i < drop; ++i) m &= ws.word((uint32_t)w * drop + i);
+          base.w[w] &= ~m;
+        }
+      }
+    }
+    if (crash_on) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const uint64_t half = ws.word((uint32_t)W * drop + (uint32_t)w);
+        base.w[w] &= ~(CB.w[w] | (CN.w[w] & ~half));
+      }
+    }
+    if (self_bit) mset(base, pid);
+    if (ho_min >= 0 && mpopc(base) <= ho_min) base = full;
+    return base;
+  }
+};
+
+// ---------------------------------------------------------------- per-instance checks
+struct Checks {
+  uint32_t ff[PSG_MAX_CHECKS];
+  uint32_t term;
+  PSG_DEV void reset() {
+#pragma unroll
+    for (int i = 0; i < PSG_MAX_CHECKS; ++i) ff[i] = PSG_NEVER;
+    term = PSG_NEVER;
+  }
+  PSG_DEV void note(int slot, bool ok, int c) {
+    if (!ok && ff[slot] == PSG_NEVER) ff[slot] = (uint32_t)c;
+  }
+  PSG_DEV void note_term(bool t, int c) {
+    if (t && term == PSG_NEVER) term = (uint32_t)c;
+  }
+};
+
+// Block-level accumulators in LDS, flushed once per block.
+struct BlockCounters {
+  unsigned int fail[PSG_MAX_CHECKS];
+  unsigned int decided;
+  unsigned int hist[PSG_MAX_ROUNDS + 2];
+  unsigned long long digest;
+};
+
+PSG_DEV void counters_init(BlockCounters* bc) {
+  for (int i = threadIdx.x; i < PSG_MAX_CHECKS; i += blockDim.x) bc->fail[i] = 0;
+  for (int i = threadIdx.x; i < PSG_MAX_ROUNDS + 2; i += blockDim.x) bc->hist[i] = 0;
+  if (threadIdx.x == 0) {
+    bc->decided = 0;
+    bc->digest = 0;
+  }
+}
+
+PSG_DEV void counters_flush(BlockCounters* bc, unsigned long long* g, int nchecks, int R) {
+  for (int i = threadIdx.x; i < nchecks; i += blockDim.x)
+    if (bc->fail[i]) atomicAdd(&g[C_FAIL + i], (unsigned long long)bc->fail[i]);
+  for (int i = threadIdx.x; i < R + 2; i += blockDim.x)
+    if (bc->hist[i]) atomicAdd(&g[C_HIST + i], (unsigned long long)bc->hist[i]);
+  if (threadIdx.x == 0) {
+    atomicAdd(&g[C_DECIDED], (unsigned long long)bc->decided);
+    atomicAdd(&g[C_DIGEST], bc->digest);
+  }
+}
+
+// Per-instance epilogue: digest, decide results, summaries, counters.
+// Called by every lane of the group; lane values are this process's results.
+template <int W>
+PSG_DEV void finish_instance(Grp<W>& g, const KArgs& a, uint64_t i, const Checks& ck, int nchecks, int32_t dec_val,
+                             int32_t dec_round, int32_t halt_round, int32_t main_x, BlockCounters* bc) {
+  const int n = a.n;
+  const bool decided = dec_round >= 0;
+  const uint64_t d = g.valid ? proc_digest(g.pid, dec_val, dec_round, halt_round, main_x) : 0ull;
+  const uint64_t dig = g.sum64(d);
+  const int nd = mpopc(g.ballot(decided));
+  if (g.valid) {
+    const uint64_t off = i * (uint64_t)n + (uint64_t)g.pid;
+    if (a.out_decision) a.out_decision[off] = dec_val;
+    if (a.out_dround) a.out_dround[off] = decided ? (uint8_t)dec_round : (uint8_t)0xFF;
+    if (a.out_rec) {
+      psg_process_record r;
+      r.decision = dec_val;
+      r.decision_round = dec_round;
+      r.halt_round = halt_round;
+      r.final_x = main_x;
+      a.out_rec[off] = r;
+    }
+  }
+  if (g.pid == 0) {
+    if (a.out_inst) {
+      psg_instance_summary s;
+      s.digest = dig;
+#pragma unroll
+      for (int c = 0; c < PSG_MAX_CHECKS; ++c) s.first_fail[c] = (uint8_t)ck.ff[c];
+      s.term_round = (uint8_t)ck.term;
+      s.n_checks = (uint8_t)nchecks;
+      s.n_decided = (uint16_t)nd;
+      a.out_inst[i] = s;
+    }
+    for (int c = 0; c < nchecks; ++c)
+      if (ck.ff[c] != PSG_NEVER) atomicAdd(&bc->fail[c], 1u);
+    atomicAdd(&bc->hist[ck.term == PSG_NEVER ? a.R + 1 : ck.term], 1u);
+    atomicAdd(&bc->decided, (unsigned int)nd);
+    atomicAdd(&bc->digest, (unsigned long long)dig);
+  }
+}
+
+// Group geometry: W == 1 -> 4 independent instances per 256-thread block;
+// W > 1 -> one instance per block of 64*W threads.
+template <int W>
+struct Geometry {
+  static constexpr int kThreads = W == 1 ? 256 : 64 * W;
+  static constexpr int kGroups = W == 1 ? 4 : 1;
+};
+
+template <int W>
+PSG_DEV void grp_setup(Grp<W>& g, const KArgs& a, uint64_t* xb, int64_t* red) {
+  g.lane = threadIdx.x & 63;
+  g.wv = W == 1 ? 0 : (threadIdx.x >> 6);
+  g.pid = g.wv * 64 + g.lane;
+  g.valid = g.pid < a.n;
+  g.ph = 0;
+  g.xb = xb;
+  g.red = red;
+}
+
+// Shared by FloodMin and KSet: slot 0 KAgreement (|{decisions of correct
+// deciders}| <= k), slot 1 KValidity (every decision is an initial value).
+template <int W>
+PSG_DEV void kagree_check(Grp<W>& g, Checks& ck, int c, int kk, const Mask<W>& full, bool decided, int32_t decision,
+                          int32_t x0, bool crashed, const int32_t* dstaged) {
+  Mask<W> Y = g.ballot(decided && !crashed);
+  int distinct = 0;
+  while (many(Y) && distinct <= kk) {
+    const int32_t dv = g.bcast(decision, dstaged, mfirst(Y));
+    Y = mandn(Y, g.ballot(decided && !crashed && decision == dv));
+    ++distinct;
+  }
+  Mask<W> Dm = g.ballot(decided);
+  bool valid = true;
+  while (valid && many(Dm)) {
+    const int32_t dv = g.bcast(decision, dstaged, mfirst(Dm));
+    Dm = mandn(Dm, g.ballot(decided && decision == dv));
+    valid = g.any(x0 == dv);
+  }
+  ck.note(0, distinct <= kk, c);
+  ck.note(1, valid, c);
+  ck.note_term(meq(g.ballot(decided), full), c);
+}
+
+
+}  // namespace psg

@@ -1,0 +1,131 @@
+// psg_floodmin.hip — FloodMin on gfx950.
+//
+// Reference: example/FloodMin.scala:8-36. x = mailbox.foldLeft(x)(min) is
+// computed without touching every sender: the distinct sender values are
+// visited in ascending order (group min-reduction), and a process resolves at
+// the first value v whose sender set E_v intersects its mailbox (or v >= x).
+// Values only decrease and converge, so one or two passes are typical.
+// Spec: TrivialSpec (FloodMin.scala:40); the build checks k-agreement with
+// k = 1 over correct processes and validity (decisions are initial values).
+#include "psg_device.hpp"
+#include "psg_kernels.hpp"
+
+namespace psg {
+
+template <int W>
+struct FmLds {
+  int32_t ds[W > 1 ? 64 * W : 1];
+};
+
+template <int W>
+__global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a) {
+  __shared__ BlockCounters bc;
+  __shared__ uint64_t xb[2 * W];
+  __shared__ int64_t red[2 * W];
+  __shared__ FmLds<W> L;
+  counters_init(&bc);
+  __syncthreads();
+  Grp<W> g;
+  grp_setup(g, a, xb, red);
+  constexpr int G = Geometry<W>::kGroups;
+  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int n = a.n;
+  const int f = a.param;
+  const Mask<W> full = mfull<W>(n);
+
+  for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
+    const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
+    Sched<W> sc;
+    sc.setup(a, inst, g.pid, g.valid);
+    const bool crashed = sc.crash_round >= 0;
+    int32_t x0 = 0;
+    if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_FLOODMIN);
+    int32_t x = x0, decision = 0;
+    bool decided = false, halted = false;
+    int32_t dec_val = 0, dec_round = -1, halt_round = -1;
+    Checks ck;
+    ck.reset();
+    auto check = [&](int c) {
+      if constexpr (W > 1) {
+        L.ds[g.pid] = decision;
+        __syncthreads();
+      }
+      kagree_check<W>(g, ck, c, 1, full, decided, decision, x0, crashed, L.ds);
+    };
+    check(0);
+    for (int k = 0; k < a.R; ++k) {
+      const Mask<W> act = g.ballot(!halted);
+      if (many(act)) {
+        Mask<W> goodS;
+        const bool good = sc.good_round(k, goodS);
+        Mask<W> CB = mzero<W>(), CN = mzero<W>();
+        if (sc.crash_on) {
+          CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
+          CN = g.ballot(sc.crash_round == k);
+        }
+        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+        // x = min(x, min{x_q : q in M}) by ascending distinct sender values
+        bool unres = !halted;
+        int32_t nx = x;
+        Mask<W> rem = act;
+        while (many(rem) && g.any(unres)) {
+          const int32_t v = g.min32(x, mtest(rem, g.pid));  // rem non-empty: v is a sender value
+          const Mask<W> E = mand(g.ballot(x == v), rem);
+          rem = mandn(rem, E);
+          if (unres) {
+            if (v >= x) {
+              unres = false;
+            } else if (many(mand(M, E))) {
+              nx = v;
+              unres = false;
+            }
+          }
+        }
+        if (!halted) {
+          x = nx;
+          const bool decideNow = a.variant == 1 ? (k >= f) : (k > f);  // FloodMin.scala:27 (variant 1: mutation)
+          if (decideNow) {
+            dec_val = x;
+            dec_round = k;
+            decided = true;
+            decision = x;
+            halt_round = k;
+            halted = true;
+          }
+        }
+      }
+      check(k + 1);
+    }
+    finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, x, &bc);
+  }
+  __syncthreads();
+  counters_flush(&bc, a.counters, 2, a.R);
+}
+
+template <int W>
+static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(floodmin_kernel<W>, dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_floodmin(const KArgs& a, int W, int grid, hipStream_t s) {
+  switch (W) {
+    case 1: return launch_w<1>(a, grid, s);
+    case 2: return launch_w<2>(a, grid, s);
+    case 3: return launch_w<3>(a, grid, s);
+    case 4: return launch_w<4>(a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+const void* floodmin_kernel_ptr(int W) {
+  switch (W) {
+    case 1: return (const void*)floodmin_kernel<1>;
+    case 2: return (const void*)floodmin_kernel<2>;
+    case 3: return (const void*)floodmin_kernel<3>;
+    case 4: return (const void*)floodmin_kernel<4>;
+  }
+  return nullptr;
+}
+
+}  // namespace psg

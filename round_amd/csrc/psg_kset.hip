@@ -1,0 +1,239 @@
+// psg_kset.hip — KSetAgreement on gfx950.
+//
+// Reference: example/KSetAgreement.scala:21-68. The state t: Map[ProcessID,Int]
+// only ever holds entries (q -> initialValue_q) (init `Map(id -> v)` at 30,
+// merge `a ++ b` at 36-38), so it is exactly a set of origins over the fixed
+// initial vector: a W x 64-bit mask per process; `t == t'` is mask equality,
+// `t ++ t'` is OR, pick(t) = min of the initial values of the origins (40).
+// Payloads (decider, t) are staged in LDS; each process walks the alive senders
+// with broadcast LDS reads. `content.find(_._1)` (53) takes the first decider
+// message in Scala Map iteration order (CHAMP for > 4 entries).
+#include "psg_device.hpp"
+#include "psg_kernels.hpp"
+
+namespace psg {
+
+template <int W>
+struct KsLds {
+  static constexpr int G = Geometry<W>::kGroups;
+  uint64_t ts[G][64 * W * W];  // staged t masks [pid][word]
+  int32_t x0s[G][64 * W];      // initial values (for pick)
+  int32_t ds[G][64 * W];       // staged decisions (spec)
+};
+
+template <int W>
+PSG_DEV void lds_fence() {
+  if constexpr (W > 1) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// pick(t) = t.values.min over the staged initial values
+template <int W>
+PSG_DEV int32_t kset_pick(const Mask<W>& t, const int32_t* x0s) {
+  int32_t m = INT32_MAX;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    uint64_t b = t.w[w];
+    while (b) {
+      const int q = w * 64 + __builtin_ctzll(b);
+      b &= b - 1;
+      m = min(m, x0s[q]);
+    }
+  }
+  return m;
+}
+
+template <int W>
+PSG_DEV Mask<W> load_t(const uint64_t* ts, int q) {
+  Mask<W> m;
+#pragma unroll
+  for (int w = 0; w < W; ++w) m.w[w] = ts[q * W + w];
+  return m;
+}
+
+template <int W>
+__global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
+  __shared__ BlockCounters bc;
+  __shared__ uint64_t xb[2 * W];
+  __shared__ int64_t red[2 * W];
+  __shared__ KsLds<W> L;
+  counters_init(&bc);
+  __syncthreads();
+  Grp<W> g;
+  grp_setup(g, a, xb, red);
+  constexpr int G = Geometry<W>::kGroups;
+  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int n = a.n;
+  const int kk = a.param;
+  const int need = a.variant == 1 ? n / 2 : n - kk;  // same.size > n - k (KSetAgreement.scala:56)
+  const Mask<W> full = mfull<W>(n);
+  uint64_t* ts = L.ts[grp];
+  int32_t* x0s = L.x0s[grp];
+  int32_t* ds = L.ds[grp];
+
+  for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
+    const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
+    Sched<W> sc;
+    sc.setup(a, inst, g.pid, g.valid);
+    const bool crashed = sc.crash_round >= 0;
+    int32_t x0 = 0;
+    if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_KSET);
+    x0s[g.pid] = x0;
+    // t = Map(id -> io.initialValue); decider = false (KSetAgreement.scala:27-31)
+    Mask<W> t = mzero<W>();
+    if (g.valid) mset(t, g.pid);
+    bool decider = false, decided = false, halted = false;
+    int32_t decision = 0, dec_val = 0, dec_round = -1, halt_round = -1;
+    Checks ck;
+    ck.reset();
+    auto check = [&](int c) {
+      ds[g.pid] = decision;
+      lds_fence<W>();
+      kagree_check<W>(g, ck, c, kk, full, decided, decision, x0, crashed, ds);
+    };
+    check(0);
+    for (int k = 0; k < a.R; ++k) {
+      const Mask<W> act = g.ballot(!halted);
+      if (many(act)) {
+        Mask<W> goodS;
+        const bool good = sc.good_round(k, goodS);
+        Mask<W> CB = mzero<W>(), CN = mzero<W>();
+        if (sc.crash_on) {
+          CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
+          CN = g.ballot(sc.crash_round == k);
+        }
+        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+        const Mask<W> Dm = mand(g.ballot(decider), act);  // senders' decider flags (pre-state)
+#pragma unroll
+        for (int w = 0; w < W; ++w) ts[g.pid * W + w] = t.w[w];
+        lds_fence<W>();
+        const Mask<W> cand = mand(M, Dm);
+        const bool isDec = decider;
+        const bool adopt = !halted && !isDec && many(cand);
+        const bool mergep = !halted && !isDec && !many(cand);
+        Mask<W> tnew = t;
+        bool becomeDecider = false;
+        if (g.any(mergep)) {
+          // same = mailbox.filter(_._2._2 == t); union of all received t
+          int same = 0;
+          Mask<W> uni = t;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            uint64_t m = act.w[w];
+            while (m) {
+              const int q = w * 64 + __builtin_ctzll(m);
+              m &= m - 1;
+              const Mask<W> tq = load_t<W>(ts, q);
+              if (mtest(M, q)) {
+                same += meq(tq, t) ? 1 : 0;
+                uni = mor(uni, tq);
+              }
+            }
+          }
+          if (mergep) {
+            if (same > need) becomeDecider = true;
+            else tnew = uni;
+          }
+        }
+        if (adopt) {
+          // t = content.find(_._1).get._2 — first decider message in iteration order
+          int qs = mfirst(cand);
+          if (a.tiebreak == PSG_TIE_CHAMP && mpopc(M) > 4 && mpopc(cand) > 1) {
+            const Mask<W> t0 = load_t<W>(ts, qs);
+            bool differ = false;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+              uint64_t m = cand.w[w];
+              while (m) {
+                const int q = w * 64 + __builtin_ctzll(m);
+                m &= m - 1;
+                if (!meq(load_t<W>(ts, q), t0)) differ = true;
+              }
+            }
+            if (differ) {
+              uint64_t best = ~0ull;
+#pragma unroll
+              for (int w = 0; w < W; ++w) {
+                uint64_t m = cand.w[w];
+                while (m) {
+                  const int q = w * 64 + __builtin_ctzll(m);
+                  m &= m - 1;
+                  const uint32_t hq = scala_improve((uint32_t)q);
+                  int depth = 0;
+#pragma unroll
+                  for (int v = 0; v < W; ++v) {
+                    uint64_t mm = M.w[v];
+                    while (mm) {
+                      const int f = v * 64 + __builtin_ctzll(mm);
+                      mm &= mm - 1;
+                      if (f != q) depth = max(depth, champ_cpl(hq, scala_improve((uint32_t)f)));
+                    }
+                  }
+                  const uint64_t key = champ_key(hq, depth);
+                  if (key < best) {
+                    best = key;
+                    qs = q;
+                  }
+                }
+              }
+            }
+          }
+          tnew = load_t<W>(ts, qs);
+          becomeDecider = true;
+        }
+        if (!halted && isDec) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:119-121)
+          const int32_t v = kset_pick<W>(t, x0s);
+          dec_val = v;
+          dec_round = k;
+          decided = true;
+          decision = v;
+          halt_round = k;
+        }
+        lds_fence<W>();  // all reads of ts done before the next round restages it
+        if (!halted) {
+          t = tnew;
+          if (becomeDecider) decider = true;
+        }
+        if (halt_round == k) halted = true;
+      }
+      check(k + 1);
+    }
+    const int32_t mainx = g.valid ? kset_pick<W>(t, x0s) : 0;
+    finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, mainx, &bc);
+    lds_fence<W>();
+  }
+  __syncthreads();
+  counters_flush(&bc, a.counters, 2, a.R);
+}
+
+template <int W>
+static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(kset_kernel<W>, dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_kset(const KArgs& a, int W, int grid, hipStream_t s) {
+  switch (W) {
+    case 1: return launch_w<1>(a, grid, s);
+    case 2: return launch_w<2>(a, grid, s);
+    case 3: return launch_w<3>(a, grid, s);
+    case 4: return launch_w<4>(a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+const void* kset_kernel_ptr(int W) {
+  switch (W) {
+    case 1: return (const void*)kset_kernel<1>;
+    case 2: return (const void*)kset_kernel<2>;
+    case 3: return (const void*)kset_kernel<3>;
+    case 4: return (const void*)kset_kernel<4>;
+  }
+  return nullptr;
+}
+
+}  // namespace psg

@@ -1,0 +1,142 @@
+"""ctypes binding of round_amd/libpsg.so (the HIP product library, include/psg.h).
+
+There is no CPU fallback: if the library is missing or no HIP device is
+present, construction raises. The library is built in-tree by
+`make -C round_amd/csrc` (or __graft_entry__.build()).
+
+Note on the HIP runtime: libpsg.so links libamdhip64.so.7. When the process
+also uses PyTorch (bench.py: torch.distributed over RCCL), import torch BEFORE
+this module so that the dynamic linker binds libpsg.so to the HIP runtime
+torch already loaded (same SONAME), keeping one HIP runtime per process.
+"""
+import ctypes as C
+import os
+import sys
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpsg.so")
+
+EXPORTED_SYMBOLS = [
+    "psg_config_default", "psg_check_count", "psg_check_name", "psg_alg_from_class",
+    "psg_create", "psg_load_inputs", "psg_run_batch", "psg_copy_decisions",
+    "psg_fetch_instances", "psg_last_error", "psg_destroy", "psg_create_error",
+]
+
+
+class PsgError(RuntimeError):
+    def __init__(self, rc, msg):
+        super().__init__(f"psg error {rc}: {msg}")
+        self.rc = rc
+
+
+_lib = None
+
+
+def load():
+    """Load libpsg.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PsgError(abi.PSG_ENODEV, f"{LIB_PATH} not built (run make -C round_amd/csrc)")
+    L = C.CDLL(LIB_PATH)
+    L.psg_config_default.argtypes = [C.POINTER(abi.Config), C.c_int32, C.c_int32]
+    L.psg_check_count.argtypes = [C.c_int32]
+    L.psg_check_name.argtypes = [C.c_int32, C.c_int32]
+    L.psg_check_name.restype = C.c_char_p
+    L.psg_alg_from_class.argtypes = [C.c_char_p]
+    L.psg_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(abi.Config)]
+    L.psg_load_inputs.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_int32)]
+    L.psg_run_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(abi.Summary),
+                                C.POINTER(abi.InstanceSummary)]
+    L.psg_copy_decisions.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    L.psg_fetch_instances.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t,
+                                      C.POINTER(abi.InstanceSummary), C.POINTER(abi.ProcessRecord)]
+    L.psg_last_error.argtypes = [C.c_void_p]
+    L.psg_last_error.restype = C.c_char_p
+    L.psg_destroy.argtypes = [C.c_void_p]
+    L.psg_destroy.restype = None
+    L.psg_create_error.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+class Context:
+    """One psg_ctx (one HIP device)."""
+
+    def __init__(self, cfg: abi.Config):
+        L = load()
+        self.cfg = cfg
+        h = C.c_void_p()
+        rc = L.psg_create(C.byref(h), C.byref(cfg))
+        if rc != 0:
+            raise PsgError(rc, L.psg_create_error().decode())
+        self._h = h
+        self._last_count = 0
+
+    def _check(self, rc):
+        if rc != 0:
+            raise PsgError(rc, load().psg_last_error(self._h).decode())
+
+    def load_inputs(self, inst_begin, count, init=None):
+        arr = None
+        if init is not None:
+            flat = [int(v) for row in init for v in row]
+            if len(flat) != count * self.cfg.n:
+                raise ValueError("init must be [count][n]")
+            arr = (C.c_int32 * len(flat))(*flat)
+        self._check(load().psg_load_inputs(self._h, inst_begin, count, arr))
+
+    def run_batch(self, inst_begin, count, per_instance=False):
+        s = abi.Summary()
+        pi = (abi.InstanceSummary * count)() if per_instance else None
+        self._check(load().psg_run_batch(self._h, inst_begin, count, C.byref(s), pi))
+        self._last_count = count
+        return s, (list(pi) if pi is not None else None)
+
+    def copy_decisions(self):
+        cells = self._last_count * self.cfg.n
+        dec = (C.c_int32 * cells)()
+        dr = (C.c_int32 * cells)()
+        self._check(load().psg_copy_decisions(self._h, dec, dr))
+        return list(dec), list(dr)
+
+    def fetch(self, ids):
+        k = len(ids)
+        arr = (C.c_uint64 * k)(*ids)
+        sums = (abi.InstanceSummary * k)()
+        recs = (abi.ProcessRecord * (k * self.cfg.n))()
+        self._check(load().psg_fetch_instances(self._h, arr, k, sums, recs))
+        return list(sums), list(recs)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().psg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def check_names(alg):
+    L = load()
+    return [L.psg_check_name(alg, i).decode() for i in range(L.psg_check_count(alg))]
+
+
+def loaded_path():
+    """Absolute path of the loaded libpsg.so (for diagnostics)."""
+    load()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if line.rstrip().endswith("libpsg.so"):
+                return line.split()[-1]
+    return None
+
+
+if __name__ == "__main__":  # pragma: no cover
+    print(loaded_path(), file=sys.stderr)

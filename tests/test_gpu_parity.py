@@ -1,0 +1,149 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Every comparison is bit-exact: per-instance summaries (digest of every
+process's decision / decision round / halt round / final state, first failing
+check point of every Spec slot, termination round), batch counters,
+per-process decide results and fetched per-process records.
+"""
+import pytest
+
+from round_amd import abi, psync
+
+pytestmark = pytest.mark.gpu
+
+H = psync.HOSchedule
+
+# (id, algorithm, n, instances, make_config kwargs)
+CASES = [
+    ("otr-c1-n4", psync.OTR(), 4, 1000, dict(rounds=10, value_range=4, seed=1)),
+    ("otr-n64-V64", psync.OTR(), 64, 2000, dict(value_range=64, seed=2)),
+    ("otr-n64-V2", psync.OTR(), 64, 2000, dict(value_range=2, seed=3)),
+    ("otr-n64-V4-after3", psync.OTR(afterDecision=3), 64, 1000, dict(value_range=4, seed=4)),
+    ("otr-n17-ragged", psync.OTR(), 17, 2000, dict(value_range=5, seed=5)),
+    ("otr-n100-W2", psync.OTR(), 100, 300, dict(value_range=8, seed=6)),
+    ("otr-n200-W4", psync.OTR(), 200, 100, dict(value_range=3, seed=6)),
+    ("otr-n1", psync.OTR(), 1, 100, dict(value_range=3, seed=7)),
+    ("otr-mutant-n8", psync.OTR(variant=1), 8, 3000, dict(schedule=H(drop_log2=1, good_round=0.0), seed=8)),
+    ("otr-pureho", psync.OTR(), 12, 2000, dict(schedule=H(drop_log2=2, self_bit=False), seed=9)),
+    ("otr-crash", psync.OTR(), 64, 500, dict(schedule=H(drop_log2=3, crash_fmax=20), seed=10)),
+    ("lv-n64-crash", psync.LastVoting(), 64, 2000, dict(seed=11)),
+    ("lv-n64-minpid", psync.LastVoting(), 64, 1000, dict(seed=12, tiebreak=abi.PSG_TIE_MIN_PID)),
+    ("lv-n5", psync.LastVoting(), 5, 3000, dict(seed=13, value_range=4)),
+    ("lv-n64-loss", psync.LastVoting(), 64, 1000, dict(seed=14, value_range=3,
+                                                      schedule=H(drop_log2=1, good_round=0.0))),
+    ("lv-mutant-n6", psync.LastVoting(variant=1), 6, 3000, dict(seed=15, value_range=5)),
+    ("lv-n130-W3", psync.LastVoting(), 130, 100, dict(seed=16)),
+    ("fm-n256-f4", psync.FloodMin(4), 256, 300, dict(seed=17)),
+    ("fm-n64-f8", psync.FloodMin(8), 64, 1000, dict(seed=18)),
+    ("fm-mutant-n16", psync.FloodMin(3, variant=1), 16, 2000, dict(seed=19)),
+    ("fm-n256-loss", psync.FloodMin(2), 256, 100, dict(seed=20, schedule=H(drop_log2=2, crash_fmax=2))),
+    ("kset-n256-k2", psync.KSetAgreement(2), 256, 24, dict(seed=21)),
+    ("kset-n64-k3-crash", psync.KSetAgreement(3), 64, 400, dict(seed=22, schedule=H(drop_log2=0, crash_fmax=10,
+                                                                                       good_round=0.0))),
+    ("kset-n16-loss", psync.KSetAgreement(2), 16, 2000, dict(seed=23, schedule=H(drop_log2=2, good_round=0.0))),
+    ("kset-n16-minpid", psync.KSetAgreement(2), 16, 2000, dict(seed=24, tiebreak=abi.PSG_TIE_MIN_PID,
+                                                              schedule=H(drop_log2=2, good_round=0.0))),
+    ("benor-n128", psync.BenOr(), 128, 300, dict(seed=25)),
+    ("benor-n4", psync.BenOr(), 4, 3000, dict(seed=26)),
+    ("benor-n64-mutant", psync.BenOr(variant=1), 64, 500, dict(seed=27)),
+    ("benor-n200-W4", psync.BenOr(), 200, 60, dict(seed=28, rounds=20)),
+]
+
+
+def _cmp_summary(g, o, rounds):
+    assert g.instances == o.instances
+    assert g.process_rounds == o.process_rounds
+    assert list(g.fail_count) == list(o.fail_count)
+    assert g.decided_processes == o.decided_processes
+    assert g.digest == o.digest
+    assert list(g.term_hist)[: rounds + 2] == list(o.term_hist)[: rounds + 2]
+
+
+def _inst_tuple(s):
+    return (s.digest, tuple(s.first_fail), s.term_round, s.n_checks, s.n_decided)
+
+
+def _rec_tuple(r):
+    return (r.decision, r.decision_round, r.halt_round, r.final_x)
+
+
+@pytest.mark.parametrize("cid,alg,n,count,kw", CASES, ids=[c[0] for c in CASES])
+def test_gpu_matches_oracle(cid, alg, n, count, kw, oracle_mod):
+    begin = 1000  # non-zero instance ids
+    with psync.GpuRound(alg, n, batch_capacity=count, **kw) as gr:
+        res = gr.run(begin, count, per_instance=True)
+        dec, dround = gr.decisions()
+        sample = [begin + i for i in range(0, count, max(1, count // 37))]
+        fsums, frecs = gr.fetch(sample)
+    cfg = gr.cfg
+    osum, opi, orec = oracle_mod.run(cfg, begin, count, per_instance=True, records=True, threads=8)
+    _cmp_summary(res.summary, osum, cfg.rounds)
+    mism = [i for i in range(count) if _inst_tuple(res.per_instance[i]) != _inst_tuple(opi[i])]
+    assert not mism, f"{len(mism)} instance summaries differ, first {mism[:5]}"
+    for i in range(count):
+        for p in range(n):
+            r = orec[i * n + p]
+            assert dec[i * n + p] == r.decision and dround[i * n + p] == r.decision_round, (i, p)
+    for j, inst in enumerate(sample):
+        i = inst - begin
+        assert _inst_tuple(fsums[j]) == _inst_tuple(opi[i])
+        for p in range(n):
+            assert _rec_tuple(frecs[j * n + p]) == _rec_tuple(orec[i * n + p]), (inst, p)
+
+
+def test_host_supplied_inputs(oracle_mod):
+    """psg_load_inputs with caller-provided initial values (ConsensusIO.initialValue)."""
+    n, count = 64, 200
+    init = [[(i * 7 + p * 13) % 5 + 1 for p in range(n)] for i in range(count)]
+    with psync.GpuRound(psync.OTR(), n, seed=31, batch_capacity=count) as gr:
+        gr.load_inputs(50, count, init)
+        res = gr.run(50, count, per_instance=True)
+    osum, opi, _ = oracle_mod.run(gr.cfg, 50, count, init=init, per_instance=True)
+    _cmp_summary(res.summary, osum, gr.cfg.rounds)
+    assert [_inst_tuple(s) for s in res.per_instance] == [_inst_tuple(s) for s in opi]
+
+
+def test_sharding_invariance_and_determinism():
+    """Any split of the instance range gives the same node-level sums (RNG keyed on global ids)."""
+    n, N = 64, 200_000
+    with psync.GpuRound(psync.OTR(), n, value_range=64, seed=41, batch_capacity=N) as gr:
+        whole = gr.run(0, N).summary
+        again = gr.run(0, N).summary
+        a = gr.run(0, N // 3).summary
+        b = gr.run(N // 3, N - N // 3).summary
+    for s in (again,):
+        assert abi.summary_to_list(s)[:-1] == abi.summary_to_list(whole)[:-1]
+    merged = [x + y for x, y in zip(abi.summary_to_list(a)[:-1], abi.summary_to_list(b)[:-1])]
+    merged = abi.summary_to_list(abi.summary_from_list(merged + [0]))[:-1]
+    assert merged == abi.summary_to_list(whole)[:-1]
+
+
+@pytest.mark.parametrize("V", [2, 4, 64])
+def test_otr_full_size_zero_false_positives(V):
+    """C2 shape at 1e6 instances: the verified OTR never violates its Spec."""
+    n, N = 64, 1_000_000
+    with psync.GpuRound(psync.OTR(), n, value_range=V, seed=100 + V, batch_capacity=N) as gr:
+        res = gr.run(0, N)
+    v = res.violations()
+    assert all(c == 0 for c in v.values()), v
+    s = res.summary
+    assert s.process_rounds == N * n * 20
+    assert sum(s.term_hist[i] for i in range(22)) == N
+
+
+def test_lastvoting_full_size_zero_false_positives():
+    n, N = 64, 500_000
+    with psync.GpuRound(psync.LastVoting(), n, seed=7, batch_capacity=N) as gr:
+        res = gr.run(0, N)
+    assert all(c == 0 for c in res.violations().values()), res.violations()
+
+
+def test_invalid_config_raises():
+    from round_amd.lib import PsgError
+    with pytest.raises((PsgError, ValueError)):
+        psync.GpuRound(psync.OTR(), 300)
+    cfg = psync.make_config(psync.OTR(), 8)
+    cfg.abi_version = 99
+    from round_amd import lib
+    with pytest.raises(PsgError):
+        lib.Context(cfg)
