@@ -26,7 +26,8 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from round_amd import abi, psync  # noqa: E402
+from round_amd import dist as rdist  # noqa: E402
+from round_amd import psync  # noqa: E402
 
 B_ALG_OTR = 24  # algorithmic bytes per process-round
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
@@ -83,7 +84,7 @@ def run_variant(rank, world, args, V, steps, warmup):
     sched = psync.HOSchedule(drop_log2=3, good_round=0.25)
     gr = psync.GpuRound(alg, args.n, rounds=args.rounds, seed=args.seed, schedule=sched, value_range=V,
                         device=dev, batch_capacity=I)
-    begin = rank * I
+    begin, _ = rdist.shard(rank, world, I)
     gr.load_inputs(begin, I)  # inputs resident in HBM before timing
     for _ in range(warmup):
         gr.run(begin, I)
@@ -100,15 +101,10 @@ def run_variant(rank, world, args, V, steps, warmup):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    # node-level result: all-reduce (sum) the int64 counters over RCCL
-    vals = abi.summary_to_list(last.summary)
-    t = torch.tensor(vals[:-1], dtype=torch.int64, device=f"cuda:{dev}")
-    tt = torch.tensor([dt, kns / max(steps, 1) / 1e9], dtype=torch.float64, device=f"cuda:{dev}")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    total = abi.summary_from_list(t.cpu().tolist() + [0])
-    dt_max, kernel_s = tt.cpu().tolist()
+    # node-level result: all-reduce (sum) the int64 counters over RCCL; max of the clocks
+    total = rdist.allreduce_summary(last.summary, device=f"cuda:{dev}")
+    dt_max = rdist.allreduce_max(dt, device=f"cuda:{dev}")
+    kernel_s = rdist.allreduce_max(kns / max(steps, 1) / 1e9, device=f"cuda:{dev}")
     cfg = gr.cfg
     gr.close()
     return {"summary": total, "dt": dt_max, "kernel_s": kernel_s, "cfg": cfg}

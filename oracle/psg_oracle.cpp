@@ -704,7 +704,7 @@ struct FloodMin {
     int32_t acc = s.x; /* mailbox.foldLeft(x)(min) */
     for (auto& m : mb) acc = std::min(acc, m.payload);
     s.x = acc;
-    bool decideNow = variant == 1 ? (k >= f) : (k > f);
+    bool decideNow = variant == 1 ? (k >= f - 1) : (k > f);
     if (decideNow) {
       cb.decide(s.x, k);
       s.decided = true; s.decision = s.x;
@@ -757,7 +757,7 @@ struct KSet {
     } else {
       int same = 0;
       for (auto& m : mb) if (*m.payload.t == s.t) ++same;
-      int need = variant == 1 ? n / 2 : n - k;
+      int need = variant == 1 ? 1 : n - k;
       if (same > need) {
         s.decider = true;
       } else {

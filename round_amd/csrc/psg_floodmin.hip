@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
         }
         if (!halted) {
           x = nx;
-          const bool decideNow = a.variant == 1 ? (k >= f) : (k > f);  // FloodMin.scala:27 (variant 1: mutation)
+          const bool decideNow = a.variant == 1 ? (k >= f - 1) : (k > f);  // FloodMin.scala:27 (variant 1: mutation)
           if (decideNow) {
             dec_val = x;
             dec_round = k;

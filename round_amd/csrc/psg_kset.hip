@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
   const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
   const int n = a.n;
   const int kk = a.param;
-  const int need = a.variant == 1 ? n / 2 : n - kk;  // same.size > n - k (KSetAgreement.scala:56)
+  const int need = a.variant == 1 ? 1 : n - kk;  // same.size > n - k (KSetAgreement.scala:56)
   const Mask<W> full = mfull<W>(n);
   uint64_t* ts = L.ts[grp];
   int32_t* x0s = L.x0s[grp];
