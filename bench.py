@@ -49,6 +49,24 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic_bytes(args):
+    """HBM bytes per launch of otr_kernel<1> from the newest committed PMC summary
+    (profiles/*/pmc_summary.json, scripts/summarize_profile.py) of this exact workload."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        w = d.get("workload", {})
+        if ("otr_kernel<1>" in d.get("kernel", "") and "hbm" in d and w.get("n") == args.n
+                and w.get("rounds") == args.rounds and w.get("instances_per_gpu") == args.instances
+                and w.get("value_range") == args.V):
+            best = (d["hbm"]["traffic_bytes"], os.path.relpath(f, ROOT))
+    return best
+
+
 def cpu_baseline(cfg, target_s):
     """Time the oracle (C++ restatement, test infrastructure) on the host cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -174,6 +192,11 @@ def main():
             },
             "variants": variants,
         }
+        tb = pmc_traffic_bytes(args)
+        if tb is not None:
+            out["roofline"]["traffic"] = tb[0] / head["kernel_s"] / 1e9
+            out["roofline"]["traffic_bytes_per_launch"] = tb[0]
+            out["roofline"]["traffic_source"] = tb[1] + " (PMC FETCH_SIZE*2 + WRITE_SIZE per launch)"
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(head["cfg"], args.cpu_seconds)
         else:

@@ -1,0 +1,82 @@
+// GpuRound.scala — Scala side of the MI355X plugin for the reference (PSync).
+//
+// Drop into the reference build as src/main/scala/psync/gpu/GpuRound.scala and
+// put libpsg_jni.so (integration/jni/psg_jni.c) + libpsg.so on java.library.path.
+// Not compiled in this repository's CI (no JVM in the image).
+//
+// It replaces, for simulation, `alg.startInstance(id, io)` on a netty Runtime
+// (psync/Algorithm.scala:36-42, psync/runtime/Runtime.scala:167-177) by a batched
+// lockstep HO execution of [begin, begin+count) instances on one GPU, with the
+// algorithm's Spec checked after every round.
+package psync.gpu
+
+import psync.Algorithm
+
+/** JNI entry points (one per psg.h function). */
+object GpuRoundNative {
+  System.loadLibrary("psg_jni")
+  @native def create(alg: Int, n: Int, rounds: Int, seed: Long, valueRange: Int, param: Int, tiebreak: Int,
+                     device: Int, variant: Int, batchCapacity: Long, dropLog2: Int, goodP32: Int, goodMin: Int,
+                     crashFmax: Int, hoMin: Int, selfBit: Boolean): Long
+  @native def loadInputs(ctx: Long, begin: Long, count: Long, init: Array[Int]): Unit
+  @native def runBatch(ctx: Long, begin: Long, count: Long, perInstance: Array[Byte]): Array[Long]
+  @native def copyDecisions(ctx: Long, decision: Array[Int], decisionRound: Array[Int]): Unit
+  @native def fetch(ctx: Long, ids: Array[Long], sums: Array[Byte], records: Array[Int]): Unit
+  @native def destroy(ctx: Long): Unit
+}
+
+/** HO schedule (faults are HO sets, psync/Process.scala:14). */
+case class HOSchedule(dropLog2: Int = 3, goodRound: Double = 0.25, goodMin: Int = -1,
+                      crashFmax: Int = -1, hoMin: Int = -1, selfBit: Boolean = true)
+
+case class GpuConfig(n: Int, rounds: Int, seed: Long = 1L, valueRange: Int = 4, param: Int = 0,
+                     schedule: HOSchedule = HOSchedule(), tiebreakChamp: Boolean = true,
+                     device: Int = 0, batchCapacity: Long = 1L << 20, variant: Int = 0)
+
+/** Node-level result of a batch (psg_summary). */
+case class GpuResult(instances: Long, processRounds: Long, failCount: Array[Long], decidedProcesses: Long,
+                     digest: Long, termHist: Array[Long], kernelNs: Long)
+
+object GpuRound {
+  /** Algorithm ids keyed on the reference class (SURVEY §8b). */
+  val registry: Map[String, Int] = Map(
+    "example.OTR" -> 1, "example.LastVoting" -> 2, "example.FloodMin" -> 3,
+    "example.KSetAgreement" -> 4, "example.BenOr" -> 5)
+
+  def algId(alg: Algorithm[_, _]): Int =
+    registry.getOrElse(alg.getClass.getName,
+      throw new IllegalArgumentException("no GPU kernel for " + alg.getClass.getName))
+
+  private def summary(a: Array[Long], rounds: Int): GpuResult = {
+    val nChecks = 12
+    GpuResult(a(0), a(1), a.slice(2, 2 + nChecks), a(2 + nChecks), a(3 + nChecks),
+              a.slice(4 + nChecks, 4 + nChecks + rounds + 2), a(a.length - 1))
+  }
+
+  /** Run instances [begin, begin+count) of `alg` in lockstep on one GPU. `init`
+    * (optional, count*n) plays ConsensusIO.initialValue; `decide` receives the
+    * ConsensusIO.decide callbacks (instance, pid, value, round) afterwards. */
+  def run(alg: Algorithm[_, _], cfg: GpuConfig, begin: Long, count: Long, init: Option[Array[Int]] = None,
+          decide: Option[(Long, Int, Int, Int) => Unit] = None): GpuResult = {
+    val s = cfg.schedule
+    val ctx = GpuRoundNative.create(algId(alg), cfg.n, cfg.rounds, cfg.seed, cfg.valueRange, cfg.param,
+      if (cfg.tiebreakChamp) 0 else 1, cfg.device, cfg.variant, cfg.batchCapacity, s.dropLog2,
+      math.min(s.goodRound * 4294967296.0, 4294967295.0).toLong.toInt, s.goodMin, s.crashFmax, s.hoMin, s.selfBit)
+    try {
+      GpuRoundNative.loadInputs(ctx, begin, count, init.orNull)
+      val res = summary(GpuRoundNative.runBatch(ctx, begin, count, null), cfg.rounds)
+      decide.foreach { cb =>
+        val cells = (count * cfg.n).toInt
+        val d = new Array[Int](cells)
+        val r = new Array[Int](cells)
+        GpuRoundNative.copyDecisions(ctx, d, r)
+        var i = 0
+        while (i < cells) {
+          if (r(i) >= 0) cb(begin + i / cfg.n, i % cfg.n, d(i), r(i))
+          i += 1
+        }
+      }
+      res
+    } finally GpuRoundNative.destroy(ctx)
+  }
+}

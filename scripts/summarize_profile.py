@@ -86,6 +86,8 @@ bench = os.path.join(args.src, "bench_default.log")
 if os.path.exists(bench):
     for line in open(bench):
         if line.startswith("{"):
-            json.dump(json.loads(line), open(os.path.join(args.dst, "bench.json"), "w"), indent=1)
+            b = json.loads(line)
+            json.dump(b, open(os.path.join(args.dst, "bench.json"), "w"), indent=1)
+            out["workload"] = {k: b["config"].get(k) for k in ("n", "rounds", "instances_per_gpu", "value_range")}
 json.dump(out, open(os.path.join(args.dst, "pmc_summary.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
