@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Throughput of the other BASELINE.json configuration rows (the headline is bench.py).
+
+  C3  LastVoting n=64, 1e8 instances over 8 GPUs (1.25e7 per GPU), 20 rounds, crash-stop
+  C4  FloodMin n=256 crash-stop sweep f in {0,1,2,4,...,64}, R = f+2; KSetAgreement n=256, k=2, R=16
+  C5  BenOr n=128, 64 rounds, |HO(p)| > n/2; termination-round histogram all-reduced
+
+One process per GPU (torchrun), weak scaling, RCCL all-reduce of the summaries.
+Prints one JSON line per configuration (rank 0). Algorithmic bytes per
+process-round per SURVEY §8d: OTR 24, LV 42, FloodMin 8, KSet 70, BenOr 11.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (first: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+from round_amd import dist as rdist  # noqa: E402
+from round_amd import psync  # noqa: E402
+
+H = psync.HOSchedule
+HBM_PEAK_GBS = 8000.0
+
+
+def configs(scale):
+    s = scale
+    out = [("C3_lastvoting_n64", psync.LastVoting(), 64, int(12_500_000 * s), {}, 42)]
+    for f in (0, 1, 2, 4, 8, 16, 32, 64):
+        out.append((f"C4_floodmin_n256_f{f}", psync.FloodMin(f), 256, int(1_000_000 * s), {}, 8))
+    out.append(("C4_kset_n256_k2", psync.KSetAgreement(2), 256, int(200_000 * s), {}, 70))
+    out.append(("C5_benor_n128", psync.BenOr(), 128, int(1_000_000 * s), {}, 11))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scale", type=float, default=1.0, help="multiply the per-GPU instance counts")
+    ap.add_argument("--only", default="", help="comma-separated name prefixes")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dev = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+    results = []
+    for name, alg, n, I, kw, balg in configs(args.scale):
+        if args.only and not any(name.startswith(p) for p in args.only.split(",")):
+            continue
+        g = psync.GpuRound(alg, n, seed=7, device=dev, batch_capacity=I, **kw)
+        begin, _ = rdist.shard(rank, world, I)
+        g.load_inputs(begin, I)
+        for _ in range(args.warmup):
+            g.run(begin, I)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        kns = 0
+        last = None
+        for _ in range(args.steps):
+            last = g.run(begin, I)
+            kns += last.summary.kernel_ns
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = rdist.allreduce_max(time.perf_counter() - t0, device=f"cuda:{dev}")
+        kern = rdist.allreduce_max(kns / args.steps / 1e9, device=f"cuda:{dev}")
+        tot = rdist.allreduce_summary(last.summary, device=f"cuda:{dev}")
+        R = g.cfg.rounds
+        g.close()
+        if rank == 0:
+            pr_launch = I * n * R
+            th = [tot.term_hist[i] for i in range(R + 2)]
+            done = sum(th[:-1])
+            rec = {
+                "config": name, "class": alg.class_name, "n": n, "rounds": R, "instances_per_gpu": I,
+                "n_gpus": world,
+                "value": tot.process_rounds * args.steps / dt, "unit": "checked process-rounds/s",
+                "kernel_ms": kern * 1e3,
+                "roofline": {"bound": "hbm", "bytes_per_process_round": balg,
+                             "achieved": pr_launch * balg / kern / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": pr_launch * balg / kern / 1e9 / HBM_PEAK_GBS},
+                "violations": psync.BatchResult(alg, R, tot).violations(),
+                "fail_count": psync.BatchResult(alg, R, tot).as_dict()["fail_count"],
+                "terminated_fraction": done / max(1, tot.instances),
+                "mean_termination_round": (sum(i * c for i, c in enumerate(th[:-1])) / done) if done else None,
+                "term_hist": th,
+            }
+            results.append(rec)
+            print(json.dumps(rec), flush=True)
+    if rank == 0 and args.out:
+        with open(args.out, "w") as f:
+            json.dump(results, f, indent=1)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

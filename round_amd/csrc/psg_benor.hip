@@ -31,12 +31,12 @@ PSG_DEV void benor_check(Grp<W>& g, Checks& ck, int c, bool has_old, int n, cons
   const Mask<W> D = g.ballot(decided);
   const bool same = !(g.any(decided && decision) && g.any(decided && !decision));
   const bool irrev = !has_old || !g.any(old_decided && !(decided && old_decision == decision));
-  ck.note(0, inv0, c);
-  ck.note(1, inv0, c);
-  ck.note(2, same, c);
-  ck.note(3, irrev, c);
-  ck.note(4, pred, c);
-  ck.note_term(meq(D, full), c);
+  const uint32_t fb = fbit(inv0, 0) |
+                      fbit(inv0, 1) |
+                      fbit(same, 2) |
+                      fbit(irrev, 3) |
+                      fbit(pred, 4);
+  ck.record(fb, meq(D, full), c, g.lane);
 }
 
 template <int W>
@@ -58,6 +58,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W> sc;
     sc.setup(a, inst, g.pid, g.valid);
+    sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_BENOR);
     // BenOrProcess state after init(io) (BenOr.scala:13-28); vote starts as None
@@ -73,7 +74,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
       bool pred = true;
       if (many(act)) {
         Mask<W> goodS;
-        const bool good = sc.good_round(k, goodS);
+        const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) {
           CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);

@@ -47,13 +47,23 @@ constexpr uint32_t COIN_TAG = 0x80000000u;
 // ---------------------------------------------------------------- Philox4x32-10
 struct U4 { uint32_t x, y, z, w; };
 
+// a ^ b ^ c in one VALU instruction: gfx950 v_bitop3_b32 with truth table 0x96
+// (hipcc otherwise emits two v_xor_b32 for the Philox mix)
+PSG_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 PSG_DEV U4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0);
+    const uint32_t n2 = xor3((uint32_t)(p0 >> 32), c3, k1);
     c1 = (uint32_t)p1;
     c3 = (uint32_t)p0;
     c0 = n0;
@@ -260,6 +270,7 @@ struct Grp {
   int pid;    // wv * 64 + lane
   bool valid; // pid < n
   int ph;
+  uint64_t vmask;  // uniform: valid lanes of this wave
   uint64_t* xb;  // LDS: [2][W] ballot words
   int64_t* red;  // LDS: [2][W] reduction words
 
@@ -269,7 +280,7 @@ struct Grp {
 
   // Mask of the processes for which pred holds (pred is ANDed with valid).
   PSG_DEV Mask<W> ballot(bool pred) {
-    const uint64_t b = __ballot(pred && valid);
+    const uint64_t b = __builtin_amdgcn_ballot_w64(pred) & vmask;
     Mask<W> m;
     if constexpr (W == 1) {
       m.w[0] = b;
@@ -404,11 +415,21 @@ struct Sched {
     return java_first_boolean(rword(seed, inst, (uint32_t)k, COIN_TAG | (uint32_t)pid, 0));
   }
 
-  // Uniform per (instance, round): good-round flag and its common HO set.
-  PSG_DEV bool good_round(int k, Mask<W>& s) const {
+  // Good rounds are uniform per (instance, round). Lane l of every wave draws
+  // round base + l in parallel (one vector Philox pass per 64 rounds) instead of
+  // a scalar-dependent draw per round; the flags become one 64-bit ballot.
+  uint64_t good_mask;
+  int good_base;
+  Mask<W> good_set;  // lane l: common HO set of round good_base + l
+
+  PSG_DEV void prep_good(int kbase, int lane, int R) {
+    good_base = kbase;
+    good_mask = 0;
+    if (good_p32 == 0) return;
+    const int k = kbase + lane;
     WordStream ws(seed, inst, (uint32_t)k, PID_GLOBAL);
-    const bool good = (uint32_t)ws.word(0) < good_p32;
-    s = full;
+    const bool good = k < R && (uint32_t)ws.word(0) < good_p32;
+    Mask<W> s = full;
     if (good && drop > 0) {
 #pragma unroll
       for (int w = 0; w < W; ++w) {
@@ -418,33 +439,63 @@ struct Sched {
       }
       if (mpopc(s) <= good_min) s = full;
     }
+    good_set = s;
+    good_mask = __builtin_amdgcn_ballot_w64(good);
+  }
+
+  PSG_DEV bool good_round(int k, int lane, int R, Mask<W>& s) {
+    if (k - good_base >= 64) prep_good(k, lane, R);
+    const int off = k - good_base;
+    const bool good = (good_mask >> off) & 1ull;
+    if (good) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) s.w[w] = readlane64(good_set.w[w], off);
+    }
     return good;
   }
 
   // HO(p) for this lane's process p in round k. CB = processes crashed before
-  // round k, CN = crashing in round k (uniform).
+  // round k, CN = crashing in round k (uniform). The random words are drawn in
+  // one straight-line pass over the Philox calls of p's stream (no divergent
+  // word cache): word j < W*drop feeds drop mask j / drop, word W*drop + w is
+  // the crash-round survival mask of word w.
   PSG_DEV Mask<W> ho(int k, int pid, bool good, const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CN) const {
-    WordStream ws(seed, inst, (uint32_t)k, (uint32_t)pid);
-    Mask<W> base;
-    if (good) {
-      base = goodS;
-    } else {
-      base = full;
-      if (drop > 0) {
+    const uint32_t nd = (uint32_t)W * drop;
+    const uint32_t j0 = good ? nd : 0u;
+    const uint32_t j1 = crash_on ? nd + (uint32_t)W : (good ? 0u : nd);
+    uint64_t dm[W], hf[W];
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-          uint64_t m = ~0ull;
-          for (uint32_t i = 0; i < drop; ++i) m &= ws.word((uint32_t)w * drop + i);
-          base.w[w] &= ~m;
+    for (int w = 0; w < W; ++w) {
+      dm[w] = ~0ull;
+      hf[w] = ~0ull;
+    }
+    for (uint32_t sidx = j0 >> 1; 2 * sidx < j1; ++sidx) {
+      const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), (uint32_t)k, (uint32_t)pid + (sidx << 16),
+                            (uint32_t)seed, (uint32_t)(seed >> 32));
+      const uint64_t wlo = (uint64_t)o.x | ((uint64_t)o.y << 32);
+      const uint64_t whi = (uint64_t)o.z | ((uint64_t)o.w << 32);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t j = 2 * sidx + (uint32_t)h;
+        const uint64_t word = h ? whi : wlo;
+        if (j < j0 || j >= j1) continue;
+        if (j < nd) {
+          const uint32_t wi = j / drop;
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            if (wi == (uint32_t)w) dm[w] &= word;
+        } else {
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            if (j - nd == (uint32_t)w) hf[w] = word;
         }
       }
     }
-    if (crash_on) {
+    Mask<W> base;
 #pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const uint64_t half = ws.word((uint32_t)W * drop + (uint32_t)w);
-        base.w[w] &= ~(CB.w[w] | (CN.w[w] & ~half));
-      }
+    for (int w = 0; w < W; ++w) {
+      base.w[w] = good ? goodS.w[w] : (drop > 0 ? full.w[w] & ~dm[w] : full.w[w]);
+      if (crash_on) base.w[w] &= ~(CB.w[w] | (CN.w[w] & ~hf[w]));
     }
     if (self_bit) mset(base, pid);
     if (ho_min >= 0 && mpopc(base) <= ho_min) base = full;
@@ -454,20 +505,33 @@ struct Sched {
 
 // ---------------------------------------------------------------- per-instance checks
 struct Checks {
-  uint32_t ff[PSG_MAX_CHECKS];
-  uint32_t term;
+  // uniform bitmask of the slots that were false at some check point, plus one
+  // VGPR whose lane s (< PSG_MAX_CHECKS) holds slot s's first failing check
+  // point and lane PSG_MAX_CHECKS the termination check point.
+  uint32_t failed;
+  bool termed;
+  int32_t ffv;
   PSG_DEV void reset() {
-#pragma unroll
-    for (int i = 0; i < PSG_MAX_CHECKS; ++i) ff[i] = PSG_NEVER;
-    term = PSG_NEVER;
+    failed = 0;
+    termed = false;
+    ffv = PSG_NEVER;
   }
-  PSG_DEV void note(int slot, bool ok, int c) {
-    if (!ok && ff[slot] == PSG_NEVER) ff[slot] = (uint32_t)c;
+  // failbits: bit s set iff slot s is false at check point c (uniform)
+  PSG_DEV void record(uint32_t failbits, bool term, int c, int lane) {
+    const uint32_t nf = failbits & ~failed;
+    if (nf) {
+      if (lane < PSG_MAX_CHECKS && ((nf >> lane) & 1u)) ffv = c;
+      failed |= nf;
+    }
+    if (term && !termed) {
+      if (lane == PSG_MAX_CHECKS) ffv = c;
+      termed = true;
+    }
   }
-  PSG_DEV void note_term(bool t, int c) {
-    if (t && term == PSG_NEVER) term = (uint32_t)c;
-  }
+  PSG_DEV uint32_t term_round() const { return (uint32_t)__builtin_amdgcn_readlane(ffv, PSG_MAX_CHECKS); }
 };
+
+PSG_DEV uint32_t fbit(bool ok, int slot) { return ok ? 0u : (1u << slot); }
 
 // Block-level accumulators in LDS, flushed once per block.
 struct BlockCounters {
@@ -520,22 +584,24 @@ PSG_DEV void finish_instance(Grp<W>& g, const KArgs& a, uint64_t i, const Checks
       a.out_rec[off] = r;
     }
   }
-  if (g.pid == 0) {
+  if (g.wv == 0) {
+    const uint32_t term = ck.term_round();
     if (a.out_inst) {
-      psg_instance_summary s;
-      s.digest = dig;
-#pragma unroll
-      for (int c = 0; c < PSG_MAX_CHECKS; ++c) s.first_fail[c] = (uint8_t)ck.ff[c];
-      s.term_round = (uint8_t)ck.term;
-      s.n_checks = (uint8_t)nchecks;
-      s.n_decided = (uint16_t)nd;
-      a.out_inst[i] = s;
+      uint8_t* o = reinterpret_cast<uint8_t*>(a.out_inst + i);
+      if (g.lane < PSG_MAX_CHECKS) o[8 + g.lane] = (uint8_t)ck.ffv;  // first_fail[lane]
+      if (g.lane == 0) {
+        *reinterpret_cast<uint64_t*>(o) = dig;
+        o[8 + PSG_MAX_CHECKS] = (uint8_t)term;
+        o[9 + PSG_MAX_CHECKS] = (uint8_t)nchecks;
+        *reinterpret_cast<uint16_t*>(o + 10 + PSG_MAX_CHECKS) = (uint16_t)nd;
+      }
     }
-    for (int c = 0; c < nchecks; ++c)
-      if (ck.ff[c] != PSG_NEVER) atomicAdd(&bc->fail[c], 1u);
-    atomicAdd(&bc->hist[ck.term == PSG_NEVER ? a.R + 1 : ck.term], 1u);
-    atomicAdd(&bc->decided, (unsigned int)nd);
-    atomicAdd(&bc->digest, (unsigned long long)dig);
+    if (g.lane < nchecks && ((ck.failed >> g.lane) & 1u)) atomicAdd(&bc->fail[g.lane], 1u);
+    if (g.lane == 0) {
+      atomicAdd(&bc->hist[term == PSG_NEVER ? a.R + 1 : term], 1u);
+      atomicAdd(&bc->decided, (unsigned int)nd);
+      atomicAdd(&bc->digest, (unsigned long long)dig);
+    }
   }
 }
 
@@ -553,6 +619,10 @@ PSG_DEV void grp_setup(Grp<W>& g, const KArgs& a, uint64_t* xb, int64_t* red) {
   g.wv = W == 1 ? 0 : (threadIdx.x >> 6);
   g.pid = g.wv * 64 + g.lane;
   g.valid = g.pid < a.n;
+  {
+    const int lo = g.wv * 64;
+    g.vmask = a.n >= lo + 64 ? ~0ull : (a.n <= lo ? 0ull : ((1ull << (a.n - lo)) - 1ull));
+  }
   g.ph = 0;
   g.xb = xb;
   g.red = red;
@@ -577,9 +647,7 @@ PSG_DEV void kagree_check(Grp<W>& g, Checks& ck, int c, int kk, const Mask<W>& f
     Dm = mandn(Dm, g.ballot(decided && decision == dv));
     valid = g.any(x0 == dv);
   }
-  ck.note(0, distinct <= kk, c);
-  ck.note(1, valid, c);
-  ck.note_term(meq(g.ballot(decided), full), c);
+  ck.record(fbit(distinct <= kk, 0) | fbit(valid, 1), meq(g.ballot(decided), full), c, g.lane);
 }
 
 

@@ -37,6 +37,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W> sc;
     sc.setup(a, inst, g.pid, g.valid);
+    sc.prep_good(0, g.lane, a.R);
     const bool crashed = sc.crash_round >= 0;
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_FLOODMIN);
@@ -57,7 +58,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
       const Mask<W> act = g.ballot(!halted);
       if (many(act)) {
         Mask<W> goodS;
-        const bool good = sc.good_round(k, goodS);
+        const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) {
           CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);

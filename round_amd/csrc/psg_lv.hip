@@ -115,14 +115,14 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, bool has_old, i
   }
   const bool integrity = !anyD || (same && d0in);
   const bool irrev = !has_old || !g.any(old_decided && !(decided && old_decision == decision));
-  ck.note(0, inv0 || inv1, c);
-  ck.note(1, inv0, c);
-  ck.note(2, inv1, c);
-  ck.note(3, same, c);
-  ck.note(4, validity, c);
-  ck.note(5, integrity, c);
-  ck.note(6, irrev, c);
-  ck.note_term(term, c);
+  const uint32_t fb = fbit(inv0 || inv1, 0) |
+                      fbit(inv0, 1) |
+                      fbit(inv1, 2) |
+                      fbit(same, 3) |
+                      fbit(validity, 4) |
+                      fbit(integrity, 5) |
+                      fbit(irrev, 6);
+  ck.record(fb, term, c, g.lane);
 }
 
 // The coordinator's HO mask (uniform).
@@ -163,6 +163,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W> sc;
     sc.setup(a, inst, g.pid, g.valid);
+    sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_LAST_VOTING);
     // LVProcess state after init(io) (LastVoting.scala:82-109)
@@ -182,7 +183,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
         const int c = phase % n;
         const bool cAlive = mtest(act, c);
         Mask<W> goodS;
-        const bool good = sc.good_round(k, goodS);
+        const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) {
           CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);

@@ -72,15 +72,15 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, Checks& ck, int c, bool has_old,
   }
   const bool integrity = !anyD || (same && d0in);
   const bool irrev = !has_old || !g.any(old_decided && !(decided && old_decision == decision));
-  ck.note(0, inv0 || inv1 || inv2, c);
-  ck.note(1, inv0, c);
-  ck.note(2, inv1, c);
-  ck.note(3, inv2, c);
-  ck.note(4, same, c);
-  ck.note(5, validity, c);
-  ck.note(6, integrity, c);
-  ck.note(7, irrev, c);
-  ck.note_term(term, c);
+  const uint32_t fb = fbit(inv0 || inv1 || inv2, 0) |
+                      fbit(inv0, 1) |
+                      fbit(inv1, 2) |
+                      fbit(inv2, 3) |
+                      fbit(same, 4) |
+                      fbit(validity, 5) |
+                      fbit(integrity, 6) |
+                      fbit(irrev, 7);
+  ck.record(fb, term, c, g.lane);
 }
 
 template <int W>
@@ -103,6 +103,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W> sc;
     sc.setup(a, inst, g.pid, g.valid);
+    sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_OTR);
     // OtrProcess state after init(io) (Otr.scala:15-26)
@@ -119,7 +120,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
       const Mask<W> act = g.ballot(!halted);
       if (many(act)) {
         Mask<W> goodS;
-        const bool good = sc.good_round(k, goodS);
+        const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) {
           CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
@@ -142,10 +143,9 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
             const Mask<W> E = mand(g.ballot(x == v), act);
             rem = mandn(rem, E);
             const int cnt = mpopc(mand(M, E));
-            if (cnt > best_c || (cnt == best_c && v < best_v)) {
-              best_c = cnt;
-              best_v = v;
-            }
+            const bool better = cnt > best_c || (cnt == best_c && v < best_v);
+            best_c = better ? cnt : best_c;
+            best_v = better ? v : best_v;
           }
           if (upd) {
             x = best_v;
