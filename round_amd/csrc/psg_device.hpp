@@ -153,6 +153,36 @@ PSG_DEV uint64_t proc_digest(int pid, int32_t dec, int32_t dround, int32_t hroun
   return splitmix64(z ^ splitmix64(y));
 }
 
+// ---------------------------------------------------------------- VALU predicates
+// Per-lane conditions as 0/1 integers in VGPRs. hipcc otherwise keeps every
+// per-lane bool as a 64-bit SGPR lane mask and evaluates && / || with scalar
+// s_and_b64/s_or_b64, which made the checker scalar-issue bound. The v_min in
+// inline asm is opaque to InstCombine, so the value stays an integer.
+PSG_DEV uint32_t nz01(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_min_u32 %0, %1, 1" : "=v"(r) : "v"(x));
+  return r;
+#else
+  return x != 0;
+#endif
+}
+PSG_DEV uint32_t ne01(int32_t a, int32_t b) { return nz01((uint32_t)(a ^ b)); }
+PSG_DEV uint32_t eq01(int32_t a, int32_t b) { return 1u - nz01((uint32_t)(a ^ b)); }
+PSG_DEV uint32_t gt01(int32_t a, int32_t b) { return (uint32_t)(((int64_t)b - (int64_t)a) >> 63) & 1u; }  // a > b
+
+// OR of a per-lane word over the wave (DPP row_shr 1/2/4/8, row_bcast 15/31),
+// returned as a uniform value (read from lane 63).
+PSG_DEV uint32_t wave_or(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // ---------------------------------------------------------------- masks
 template <int W>
 struct Mask {
@@ -334,7 +364,7 @@ struct Grp {
     for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
     return v;
   }
-  template <int OP>  // 0 min, 1 max, 2 sum
+  template <int OP>  // 0 min, 1 max, 2 sum, 3 or
   PSG_DEV int64_t cross64(int64_t v) {
     if constexpr (W == 1) {
       return v;
@@ -349,9 +379,19 @@ struct Grp {
         int64_t t = s[i];
         if (OP == 0) r = t < r ? t : r;
         else if (OP == 1) r = t > r ? t : r;
-        else r = (int64_t)((uint64_t)r + (uint64_t)t);
+        else if (OP == 2) r = (int64_t)((uint64_t)r + (uint64_t)t);
+        else r = r | t;
       }
       return r;
+    }
+  }
+  // OR of a per-lane word over the group (uniform result)
+  PSG_DEV uint32_t gor(uint32_t v) {
+    const uint32_t w = wave_or(v);
+    if constexpr (W == 1) {
+      return w;
+    } else {
+      return (uint32_t)cross64<3>((int64_t)w);
     }
   }
   PSG_DEV int64_t min64(int64_t v, bool in) { return cross64<0>(wave_min64((in && valid) ? v : INT64_MAX)); }
@@ -368,6 +408,18 @@ struct Grp {
     else return (int32_t)cross64<1>(m);
   }
 };
+
+// Make this group's LDS writes visible to the whole group (W > 1: block barrier;
+// W == 1: the wave's own LDS operations are ordered, so a wave-scope fence suffices).
+template <int W>
+PSG_DEV void lds_sync() {
+  if constexpr (W > 1) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
 
 // ---------------------------------------------------------------- schedule
 template <int W>
@@ -628,11 +680,141 @@ PSG_DEV void grp_setup(Grp<W>& g, const KArgs& a, uint64_t* xb, int64_t* red) {
   g.red = red;
 }
 
+// Set of an instance's initial values as an LDS open-addressing hash table
+// (128 slots per 64 processes, load <= 1/2), built once per instance with one
+// lane per value. Membership ("i.x == init(j.x) for some j", Validity) is then
+// one or two LDS probes per lane instead of a loop over distinct values.
+template <int W>
+struct X0Set {
+  static constexpr int kSlots = W == 1 ? 128 : (W == 2 ? 256 : 512);  // power of two >= 128 * W
+  static constexpr int32_t kEmpty = INT32_MIN;
+  int32_t* tab;
+  bool has_empty;  // the sentinel value itself is an initial value
+
+  PSG_DEV static uint32_t slot(int32_t v) {
+    constexpr int kBits = W == 1 ? 7 : (W == 2 ? 8 : 9);  // log2(kSlots)
+    return ((uint32_t)v * 0x9E3779B1u) >> (32 - kBits);
+  }
+  PSG_DEV void build(Grp<W>& g, int32_t* lds, int32_t x0) {
+    tab = lds;
+    for (int t = g.pid; t < kSlots; t += 64 * W) tab[t] = kEmpty;
+    lds_sync<W>();
+    if (g.valid && x0 != kEmpty) {
+      uint32_t h = slot(x0);
+      while (true) {
+        const int32_t prev = atomicCAS(&tab[h], kEmpty, x0);
+        if (prev == kEmpty || prev == x0) break;
+        h = (h + 1) & (uint32_t)(kSlots - 1);
+      }
+    }
+    has_empty = g.any(x0 == kEmpty);
+    lds_sync<W>();
+  }
+  // Uniform: does every process selected by `sel` hold a value of the set?
+  // Fast path: one ballot of "v is in neither of its two home slots"; the probe
+  // loop runs only for lanes that miss both (load <= 1/2 makes that rare).
+  PSG_DEV bool all_in(Grp<W>& g, const Mask<W>& sel, int32_t v) const {
+    const uint32_t h = slot(v);
+    const int32_t t0 = tab[h];
+    const int32_t t1 = tab[(h + 1) & (uint32_t)(kSlots - 1)];
+    const Mask<W> need = mand(g.ballot(t0 != v && t1 != v), sel);
+    if (!many(need)) return true;
+    return !g.any(mtest(need, g.pid) && !contains(v));
+  }
+
+  // contains() as a VALU 0/1 integer (see nz01); same probing scheme
+  PSG_DEV uint32_t contains01(int32_t v) const {
+    const uint32_t h = slot(v);
+    const int32_t t0 = tab[h];
+    const int32_t t1 = tab[(h + 1) & (uint32_t)(kSlots - 1)];
+    const uint32_t e0 = eq01(t0, v), z0 = eq01(t0, kEmpty), e1 = eq01(t1, v), z1 = eq01(t1, kEmpty);
+    uint32_t hit = e0 | ((1u - z0) & e1);
+    const uint32_t done = e0 | z0 | e1 | z1;
+    if (__builtin_amdgcn_ballot_w64(done == 0u) != 0ull) {
+      if (done == 0u) {
+        uint32_t q = (h + 2) & (uint32_t)(kSlots - 1);
+        while (true) {
+          const int32_t t = tab[q];
+          if (t == v) { hit = 1u; break; }
+          if (t == kEmpty) break;
+          q = (q + 1) & (uint32_t)(kSlots - 1);
+        }
+      }
+    }
+    const uint32_t isE = eq01(v, kEmpty);
+    return (isE & (has_empty ? 1u : 0u)) | ((1u - isE) & hit);
+  }
+  // Two adjacent slots are read unconditionally (load <= 1/2: almost every probe
+  // resolves there); the probe loop runs only if some lane is still unresolved.
+  PSG_DEV bool contains(int32_t v) const {
+    const uint32_t h = slot(v);
+    const int32_t t0 = tab[h];
+    const int32_t t1 = tab[(h + 1) & (uint32_t)(kSlots - 1)];
+    bool hit = t0 == v || (t0 != kEmpty && t1 == v);
+    const bool done = t0 == v || t0 == kEmpty || t1 == v || t1 == kEmpty;
+    if (__builtin_amdgcn_ballot_w64(!done) != 0ull) {
+      if (!done) {
+        uint32_t q = (h + 2) & (uint32_t)(kSlots - 1);
+        while (true) {
+          const int32_t t = tab[q];
+          if (t == v) { hit = true; break; }
+          if (t == kEmpty) break;
+          q = (q + 1) & (uint32_t)(kSlots - 1);
+        }
+      }
+    }
+    return v == kEmpty ? has_empty : hit;
+  }
+};
+
+// Candidate for a strict-majority value among the valid lanes of the group
+// (Boyer-Moore pair cancellation as a butterfly reduction): if some value
+// occurs more than n/2 times, it is returned; otherwise an arbitrary value.
+template <int W>
+PSG_DEV int32_t majority_candidate(Grp<W>& g, int32_t x) {
+  int32_t c = x;
+  int32_t k = g.valid ? 1 : 0;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {  // branch-free pair cancellation
+    const int32_t c2 = __shfl_xor(c, o);
+    const int32_t k2 = __shfl_xor(k, o);
+    const uint32_t same = eq01(c, c2);
+    const uint32_t keep = same | (1u - gt01(k2, k));  // c == c2 or k >= k2
+    const int32_t diff = k - k2;
+    const int32_t kn = same ? k + k2 : (diff < 0 ? -diff : diff);
+    c = keep ? c : c2;
+    k = kn;
+  }
+  if constexpr (W == 1) {
+    return rfl32(c);
+  } else {
+    int64_t* s = g.red + g.ph * W;
+    g.ph ^= 1;
+    if (g.lane == 0) s[g.wv] = ((int64_t)k << 32) | (uint32_t)c;
+    __syncthreads();
+    int32_t cc = (int32_t)(uint32_t)s[0];
+    int32_t kk = (int32_t)(s[0] >> 32);
+    for (int w = 1; w < W; ++w) {
+      const int32_t c2 = (int32_t)(uint32_t)s[w];
+      const int32_t k2 = (int32_t)(s[w] >> 32);
+      if (cc == c2) {
+        kk += k2;
+      } else if (kk >= k2) {
+        kk -= k2;
+      } else {
+        cc = c2;
+        kk = k2 - kk;
+      }
+    }
+    return rfl32(cc);
+  }
+}
+
 // Shared by FloodMin and KSet: slot 0 KAgreement (|{decisions of correct
 // deciders}| <= k), slot 1 KValidity (every decision is an initial value).
 template <int W>
 PSG_DEV void kagree_check(Grp<W>& g, Checks& ck, int c, int kk, const Mask<W>& full, bool decided, int32_t decision,
-                          int32_t x0, bool crashed, const int32_t* dstaged) {
+                          const X0Set<W>& X0, bool crashed, const int32_t* dstaged) {
   Mask<W> Y = g.ballot(decided && !crashed);
   int distinct = 0;
   while (many(Y) && distinct <= kk) {
@@ -640,13 +822,7 @@ PSG_DEV void kagree_check(Grp<W>& g, Checks& ck, int c, int kk, const Mask<W>& f
     Y = mandn(Y, g.ballot(decided && !crashed && decision == dv));
     ++distinct;
   }
-  Mask<W> Dm = g.ballot(decided);
-  bool valid = true;
-  while (valid && many(Dm)) {
-    const int32_t dv = g.bcast(decision, dstaged, mfirst(Dm));
-    Dm = mandn(Dm, g.ballot(decided && decision == dv));
-    valid = g.any(x0 == dv);
-  }
+  const bool valid = !g.any(decided && !X0.contains(decision));
   ck.record(fbit(distinct <= kk, 0) | fbit(valid, 1), meq(g.ballot(decided), full), c, g.lane);
 }
 

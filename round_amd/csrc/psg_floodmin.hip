@@ -23,6 +23,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
   __shared__ uint64_t xb[2 * W];
   __shared__ int64_t red[2 * W];
   __shared__ FmLds<W> L;
+  __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
   counters_init(&bc);
   __syncthreads();
   Grp<W> g;
@@ -41,6 +42,8 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
     const bool crashed = sc.crash_round >= 0;
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_FLOODMIN);
+    X0Set<W> X0;
+    X0.build(g, x0tab[grp], x0);
     int32_t x = x0, decision = 0;
     bool decided = false, halted = false;
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
@@ -51,7 +54,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
         L.ds[g.pid] = decision;
         __syncthreads();
       }
-      kagree_check<W>(g, ck, c, 1, full, decided, decision, x0, crashed, L.ds);
+      kagree_check<W>(g, ck, c, 1, full, decided, decision, X0, crashed, L.ds);
     };
     check(0);
     for (int k = 0; k < a.R; ++k) {

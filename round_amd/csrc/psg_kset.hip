@@ -21,16 +21,6 @@ struct KsLds {
   int32_t ds[G][64 * W];       // staged decisions (spec)
 };
 
-template <int W>
-PSG_DEV void lds_fence() {
-  if constexpr (W > 1) {
-    __syncthreads();
-  } else {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
 // pick(t) = t.values.min over the staged initial values
 template <int W>
 PSG_DEV int32_t kset_pick(const Mask<W>& t, const int32_t* x0s) {
@@ -61,6 +51,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
   __shared__ uint64_t xb[2 * W];
   __shared__ int64_t red[2 * W];
   __shared__ KsLds<W> L;
+  __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
   counters_init(&bc);
   __syncthreads();
   Grp<W> g;
@@ -84,6 +75,8 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_KSET);
     x0s[g.pid] = x0;
+    X0Set<W> X0;
+    X0.build(g, x0tab[grp], x0);
     // t = Map(id -> io.initialValue); decider = false (KSetAgreement.scala:27-31)
     Mask<W> t = mzero<W>();
     if (g.valid) mset(t, g.pid);
@@ -93,8 +86,8 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
     ck.reset();
     auto check = [&](int c) {
       ds[g.pid] = decision;
-      lds_fence<W>();
-      kagree_check<W>(g, ck, c, kk, full, decided, decision, x0, crashed, ds);
+      lds_sync<W>();
+      kagree_check<W>(g, ck, c, kk, full, decided, decision, X0, crashed, ds);
     };
     check(0);
     for (int k = 0; k < a.R; ++k) {
@@ -111,7 +104,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
         const Mask<W> Dm = mand(g.ballot(decider), act);  // senders' decider flags (pre-state)
 #pragma unroll
         for (int w = 0; w < W; ++w) ts[g.pid * W + w] = t.w[w];
-        lds_fence<W>();
+        lds_sync<W>();
         const Mask<W> cand = mand(M, Dm);
         const bool isDec = decider;
         const bool adopt = !halted && !isDec && many(cand);
@@ -194,7 +187,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
           decision = v;
           halt_round = k;
         }
-        lds_fence<W>();  // all reads of ts done before the next round restages it
+        lds_sync<W>();  // all reads of ts done before the next round restages it
         if (!halted) {
           t = tnew;
           if (becomeDecider) decider = true;
@@ -205,7 +198,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
     }
     const int32_t mainx = g.valid ? kset_pick<W>(t, x0s) : 0;
     finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, mainx, &bc);
-    lds_fence<W>();
+    lds_sync<W>();
   }
   __syncthreads();
   counters_flush(&bc, a.counters, 2, a.R);

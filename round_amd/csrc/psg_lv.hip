@@ -39,8 +39,8 @@ PSG_DEV void lv_stage(Grp<W>& g, LvLds<W>& L, int32_t x, int32_t ts, int32_t vot
 // (keepInit && (noDecision || majority)), 2 Invariant1, 3 Agreement, 4 Validity,
 // 5 Integrity, 6 Irrevocability. roundInvariants(j-1)(0) is `true` for every j.
 template <int W>
-PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, bool has_old, int n, const Mask<W>& full, int32_t x,
-                      int32_t x0, int32_t ts, int32_t vote, int32_t decision, bool decided, bool commit, bool ready,
+PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, const X0Set<W>& X0, Checks& ck, int c, bool has_old, int n,
+                      const Mask<W>& full, int32_t x, int32_t ts, int32_t vote, int32_t decision, bool decided, bool commit, bool ready,
                       bool old_decided, int32_t old_decision) {
   lv_stage<W>(g, L, x, ts, vote, decision, decided, commit, ready);
   const int32_t r4 = c / 4;
@@ -53,16 +53,8 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, bool has_old, i
     d0 = g.bcast(decision, L.ds, mfirst(D));
     same = !g.any(decided && decision != d0);
   }
-  // keepInit: P.forall(i => P.exists(j1 => i.x == init(j1.x)))
-  bool keep = true;
-  {
-    Mask<W> rem = full;
-    while (keep && many(rem)) {
-      const int32_t v = g.bcast(x, L.xs, mfirst(rem));
-      rem = mandn(rem, g.ballot(x == v));
-      keep = g.any(x0 == v);
-    }
-  }
+  // keepInit: P.forall(i => P.exists(j1 => i.x == init(j1.x))) — one X0-set probe per lane
+  const bool keep = !g.any(!X0.contains(x));
   const bool noDec = !g.any(decided || ready);
   // values pinned by (decided ==> decision == v), (commit ==> vote == v), (ready ==> vote == v)
   const Mask<W> Pm = g.ballot(decided || commit || ready);
@@ -97,22 +89,10 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, bool has_old, i
     }
   }
   const bool inv0 = keep && (noDec || maj);
-  const bool d0in = anyD && g.any(x0 == d0);
+  const bool d0in = anyD && rfl32(X0.contains(d0) ? 1 : 0) != 0;
   const bool term = meq(D, full);
   const bool inv1 = term && same && d0in;
-  bool validity = true;
-  if (anyD) {
-    if (same) {
-      validity = d0in;
-    } else {
-      Mask<W> remD = D;
-      while (many(remD)) {
-        const int32_t dv = g.bcast(decision, L.ds, mfirst(remD));
-        remD = mandn(remD, g.ballot(decided && decision == dv));
-        if (validity) validity = g.any(x0 == dv);
-      }
-    }
-  }
+  const bool validity = !g.any(decided && !X0.contains(decision));
   const bool integrity = !anyD || (same && d0in);
   const bool irrev = !has_old || !g.any(old_decided && !(decided && old_decision == decision));
   const uint32_t fb = fbit(inv0 || inv1, 0) |
@@ -148,6 +128,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
   __shared__ uint64_t xb[2 * W];
   __shared__ int64_t red[2 * W];
   __shared__ LvLds<W> L;
+  __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
   counters_init(&bc);
   __syncthreads();
   Grp<W> g;
@@ -167,12 +148,14 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_LAST_VOTING);
     // LVProcess state after init(io) (LastVoting.scala:82-109)
+    X0Set<W> X0;
+    X0.build(g, x0tab[grp], x0);
     int32_t x = x0, ts = -1, vote = 0, decision = -1;
     bool ready = false, commit = false, decided = false, halted = false;
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
     Checks ck;
     ck.reset();
-    lv_check<W>(g, L, ck, 0, false, n, full, x, x0, ts, vote, decision, decided, commit, ready, false, -1);
+    lv_check<W>(g, L, X0, ck, 0, false, n, full, x, ts, vote, decision, decided, commit, ready, false, -1);
 
     for (int k = 0; k < a.R; ++k) {
       const bool old_decided = decided;
@@ -267,7 +250,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
           }
         }
       }
-      lv_check<W>(g, L, ck, k + 1, true, n, full, x, x0, ts, vote, decision, decided, commit, ready, old_decided,
+      lv_check<W>(g, L, X0, ck, k + 1, true, n, full, x, ts, vote, decision, decided, commit, ready, old_decided,
                   old_decision);
     }
     finish_instance<W>(g, a, i, ck, 7, dec_val, dec_round, halt_round, x, &bc);

@@ -15,71 +15,50 @@ namespace psg {
 template <int W>
 struct OtrLds {
   int32_t xs[W > 1 ? 64 * W : 1];
-  int32_t x0s[W > 1 ? 64 * W : 1];
   int32_t ds[W > 1 ? 64 * W : 1];
 };
 
 // Spec check at check point c (spec r = c). Slots: 0 Safety (some invariant
 // holds), 1..3 invariants, 4 Agreement, 5 Validity, 6 Integrity, 7 Irrevocability.
+// Every formula is evaluated from scratch at every check point. The per-process
+// parts of the universally quantified formulas are computed as 0/1 VALU words and
+// OR-reduced over the wave in one DPP pass:
+//   bit 0  !(i.x == init(j.x) for some j)           keepInit   (X0-set probe)
+//   bit 1  i.decided && i.decision != d0            Agreement  (d0 = a decided value)
+//   bit 2  i.decided && i.decision not initial      Validity
+//   bit 3  old(i.decided) && !(i.decided && old(i.decision) == i.decision)  Irrevocability
+// V.exists(v => |{i : i.x == v}| > 2n/3 && all decisions == v): with decisions only
+// v = d0 can qualify; without, v must be a strict majority (Boyer-Moore candidate).
 template <int W>
-PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, Checks& ck, int c, bool has_old, int n, const Mask<W>& full,
-                       int32_t x, int32_t x0, bool decided, int32_t decision, bool old_decided, int32_t old_decision) {
+PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, int c, bool has_old, int n,
+                       const Mask<W>& full, int32_t x, uint32_t dec01, int32_t decision, uint32_t old01,
+                       int32_t old_decision, uint32_t valid01) {
   const int sthr = (2 * n) / 3;  // 2*n/3 in the Spec (Otr.scala:101)
   if constexpr (W > 1) {
-    L.xs[g.pid] = x;
     L.ds[g.pid] = decision;
     __syncthreads();
   }
-  const Mask<W> D = g.ballot(decided);
+  const Mask<W> D = g.ballot(dec01 != 0u);
   const bool anyD = many(D);
-  int32_t d0 = 0;
-  bool same = true;
-  if (anyD) {
-    d0 = g.bcast(decision, L.ds, mfirst(D));
-    same = !g.any(decided && decision != d0);
-  }
-  // V.exists(v => |{i : i.x == v}| ... ) finitized over the current x values;
-  // keepInit: P.forall(i => P.exists(j => i.x == init(j.x))).
-  Mask<W> rem = full;
-  bool e0 = false, e1 = false, keep = true;
-  while (many(rem)) {
-    const int32_t v = g.bcast(x, L.xs, mfirst(rem));
-    const Mask<W> E = g.ballot(x == v);
-    rem = mandn(rem, E);
-    if (keep) keep = g.any(x0 == v);
-    const int cnt = mpopc(E);
-    const bool condv = !anyD || (same && v == d0);
-    e0 = e0 || (cnt > sthr && condv);
-    e1 = e1 || (cnt == n && condv);
-  }
+  const int32_t d0 = anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
+  const bool keep = X0.all_in(g, full, x);                           // keepInit
+  const bool validity = X0.all_in(g, D, decision);                   // decisions are initial values
+  const bool same = !many(mand(D, g.ballot(decision != d0)));        // Agreement
+  const Mask<W> OLD = g.ballot(old01 != 0u);                         // Irrevocability
+  const bool irrev = !has_old || !many(mandn(OLD, mand(D, g.ballot(old_decision == decision))));
+  const int32_t ref = anyD ? d0 : majority_candidate<W>(g, x);
+  const int cnt = mpopc(g.ballot((valid01 & eq01(x, ref)) != 0u));
+  const bool condv = !anyD || same;
+  const bool e0 = condv && cnt > sthr;
+  const bool e1 = condv && cnt == n;
   const bool inv0 = (!anyD || e0) && keep;
   const bool inv1 = e1 && keep;
-  const bool d0in = anyD && g.any(x0 == d0);
   const bool term = meq(D, full);
-  const bool inv2 = term && same && d0in;
-  bool validity = true;
-  if (anyD) {
-    if (same) {
-      validity = d0in;
-    } else {
-      Mask<W> remD = D;
-      while (many(remD)) {
-        const int32_t dv = g.bcast(decision, L.ds, mfirst(remD));
-        remD = mandn(remD, g.ballot(decided && decision == dv));
-        if (validity) validity = g.any(x0 == dv);
-      }
-    }
-  }
-  const bool integrity = !anyD || (same && d0in);
-  const bool irrev = !has_old || !g.any(old_decided && !(decided && old_decision == decision));
-  const uint32_t fb = fbit(inv0 || inv1 || inv2, 0) |
-                      fbit(inv0, 1) |
-                      fbit(inv1, 2) |
-                      fbit(inv2, 3) |
-                      fbit(same, 4) |
-                      fbit(validity, 5) |
-                      fbit(integrity, 6) |
-                      fbit(irrev, 7);
+  const bool d0in = same && validity;  // all decisions equal d0 and are initial values
+  const bool inv2 = term && d0in;
+  const bool integrity = !anyD || d0in;
+  const uint32_t fb = fbit(inv0 || inv1 || inv2, 0) | fbit(inv0, 1) | fbit(inv1, 2) | fbit(inv2, 3) |
+                      fbit(same, 4) | fbit(validity, 5) | fbit(integrity, 6) | fbit(irrev, 7);
   ck.record(fb, term, c, g.lane);
 }
 
@@ -89,6 +68,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
   __shared__ uint64_t xb[2 * W];
   __shared__ int64_t red[2 * W];
   __shared__ OtrLds<W> L;
+  __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
   counters_init(&bc);
   __syncthreads();
   Grp<W> g;
@@ -98,6 +78,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
   const int n = a.n;
   const int thr = a.variant == 1 ? n / 2 : (2 * n) / 3;  // Otr.scala:64, 67 (variant 1: mutation)
   const Mask<W> full = mfull<W>(n);
+  const uint32_t valid01 = g.valid ? 1u : 0u;
 
   for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
@@ -106,18 +87,20 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
     sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_OTR);
-    // OtrProcess state after init(io) (Otr.scala:15-26)
+    X0Set<W> X0;
+    X0.build(g, x0tab[grp], x0);
+    // OtrProcess state after init(io) (Otr.scala:15-26); flags are 0/1 lane words
     int32_t x = x0, decision = -1, after = a.param;
-    bool decided = false, halted = false;
+    uint32_t dec01 = 0, halted01 = 1u - valid01;
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
     Checks ck;
     ck.reset();
-    otr_check<W>(g, L, ck, 0, false, n, full, x, x0, decided, decision, false, -1);
+    otr_check<W>(g, L, X0, ck, 0, false, n, full, x, dec01, decision, 0u, -1, valid01);
 
     for (int k = 0; k < a.R; ++k) {
-      const bool old_decided = decided;
+      const uint32_t old01 = dec01;
       const int32_t old_decision = decision;
-      const Mask<W> act = g.ballot(!halted);
+      const Mask<W> act = g.ballot(halted01 == 0u);
       if (many(act)) {
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
@@ -128,46 +111,42 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
         }
         // mailbox: broadcast(x) from every alive sender in HO(p)
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
-        const bool upd = !halted && mpopc(M) > thr;
-        if (g.any(upd)) {
+        const uint32_t upd = (1u - halted01) & gt01(mpopc(M), thr);
+        if (g.any(upd != 0u)) {
           if constexpr (W > 1) {
             L.xs[g.pid] = x;
             __syncthreads();
           }
           // mmor: max multiplicity, ties -> smaller value (OtrExample.scala:67-75)
           Mask<W> rem = act;
-          int best_c = 0;
+          int32_t best_c = 0;
           int32_t best_v = INT32_MAX;
           while (many(rem)) {
             const int32_t v = g.bcast(x, L.xs, mfirst(rem));
             const Mask<W> E = mand(g.ballot(x == v), act);
             rem = mandn(rem, E);
-            const int cnt = mpopc(mand(M, E));
-            const bool better = cnt > best_c || (cnt == best_c && v < best_v);
+            const int32_t cnt = mpopc(mand(M, E));
+            const uint32_t better = gt01(cnt, best_c) | (eq01(cnt, best_c) & gt01(best_v, v));
             best_c = better ? cnt : best_c;
             best_v = better ? v : best_v;
           }
-          if (upd) {
-            x = best_v;
-            if (best_c > thr) {
-              if (!decided) {  // callback.decide(v) only the first time (Otr.scala:68-70)
-                dec_val = best_v;
-                dec_round = k;
-              }
-              decided = true;
-              decision = best_v;
-            }
-          }
+          // x = mmor; decide on > 2n/3 copies, callback only the first time (Otr.scala:64-73)
+          x = upd ? best_v : x;
+          const uint32_t newdec = upd & gt01(best_c, thr);
+          const uint32_t first = newdec & (1u - dec01);
+          dec_val = first ? best_v : dec_val;
+          dec_round = first ? k : dec_round;
+          decision = newdec ? best_v : decision;
+          dec01 |= newdec;
         }
-        if (!halted && decided) {  // Otr.scala:75-80
-          after -= 1;
-          if (after <= 0) {
-            halt_round = k;
-            halted = true;  // exitAtEndOfRound
-          }
-        }
+        // after -= 1 once decided; exitAtEndOfRound when it reaches 0 (Otr.scala:75-80)
+        const uint32_t ad = (1u - halted01) & dec01;
+        after -= (int32_t)ad;
+        const uint32_t h = ad & gt01(1, after);
+        halt_round = h ? k : halt_round;
+        halted01 |= h;
       }
-      otr_check<W>(g, L, ck, k + 1, true, n, full, x, x0, decided, decision, old_decided, old_decision);
+      otr_check<W>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, old01, old_decision, valid01);
     }
     finish_instance<W>(g, a, i, ck, 8, dec_val, dec_round, halt_round, x, &bc);
   }
