@@ -12,25 +12,25 @@
 
 namespace psg {
 
+// per-process flag bits (one VGPR word; see nz01 in psg_device.hpp)
+enum : uint32_t { F_DECIDED = 1u, F_COMMIT = 2u, F_READY = 4u, F_HALTED = 8u };
+
 template <int W>
 struct LvLds {
   int32_t xs[W > 1 ? 64 * W : 1];
   int32_t tss[W > 1 ? 64 * W : 1];
   int32_t votes[W > 1 ? 64 * W : 1];
   int32_t ds[W > 1 ? 64 * W : 1];
-  int32_t flags[W > 1 ? 64 * W : 1];  // bit0 decided, bit1 commit, bit2 ready
   uint64_t hos[W > 1 ? 64 * W * W : 1];
 };
 
 template <int W>
-PSG_DEV void lv_stage(Grp<W>& g, LvLds<W>& L, int32_t x, int32_t ts, int32_t vote, int32_t decision, bool decided,
-                      bool commit, bool ready) {
+PSG_DEV void lv_stage(Grp<W>& g, LvLds<W>& L, int32_t x, int32_t ts, int32_t vote, int32_t decision) {
   if constexpr (W > 1) {
     L.xs[g.pid] = x;
     L.tss[g.pid] = ts;
     L.votes[g.pid] = vote;
     L.ds[g.pid] = decision;
-    L.flags[g.pid] = (decided ? 1 : 0) | (commit ? 2 : 0) | (ready ? 4 : 0);
     __syncthreads();
   }
 }
@@ -40,35 +40,31 @@ PSG_DEV void lv_stage(Grp<W>& g, LvLds<W>& L, int32_t x, int32_t ts, int32_t vot
 // 5 Integrity, 6 Irrevocability. roundInvariants(j-1)(0) is `true` for every j.
 template <int W>
 PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, const X0Set<W>& X0, Checks& ck, int c, bool has_old, int n,
-                      const Mask<W>& full, int32_t x, int32_t ts, int32_t vote, int32_t decision, bool decided, bool commit, bool ready,
-                      bool old_decided, int32_t old_decision) {
-  lv_stage<W>(g, L, x, ts, vote, decision, decided, commit, ready);
+                      const Mask<W>& full, int32_t x, int32_t ts, int32_t vote, int32_t decision, uint32_t fl,
+                      uint32_t old_fl, int32_t old_decision) {
+  lv_stage<W>(g, L, x, ts, vote, decision);
   const int32_t r4 = c / 4;
   const int coord = r4 % n;
-  const Mask<W> D = g.ballot(decided);
+  const Mask<W> D = g.ballot((fl & F_DECIDED) != 0u);
+  const Mask<W> C = g.ballot((fl & F_COMMIT) != 0u);
+  const Mask<W> Rd = g.ballot((fl & F_READY) != 0u);
   const bool anyD = many(D);
-  int32_t d0 = 0;
-  bool same = true;
-  if (anyD) {
-    d0 = g.bcast(decision, L.ds, mfirst(D));
-    same = !g.any(decided && decision != d0);
-  }
-  // keepInit: P.forall(i => P.exists(j1 => i.x == init(j1.x))) — one X0-set probe per lane
-  const bool keep = !g.any(!X0.contains(x));
-  const bool noDec = !g.any(decided || ready);
+  const int32_t d0 = anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
+  const bool same = !many(mand(D, g.ballot(decision != d0)));
+  const bool keep = X0.all_in(g, full, x);  // P.forall(i => P.exists(j1 => i.x == init(j1.x)))
+  const bool noDec = !many(mor(D, Rd));
   // values pinned by (decided ==> decision == v), (commit ==> vote == v), (ready ==> vote == v)
-  const Mask<W> Pm = g.ballot(decided || commit || ready);
+  const Mask<W> CR = mor(C, Rd);
+  const Mask<W> Pm = mor(D, CR);
   const bool zAny = many(Pm);
   int32_t z0 = 0;
   bool zOk = true;
   if (zAny) {
     const int q = mfirst(Pm);
-    const int32_t fq = g.bcast((decided ? 1 : 0), L.flags, q) & 1;
-    z0 = fq ? g.bcast(decision, L.ds, q) : g.bcast(vote, L.votes, q);
-    zOk = !g.any((decided && decision != z0) || ((commit || ready) && vote != z0));
+    z0 = mtest(D, q) ? g.bcast(decision, L.ds, q) : g.bcast(vote, L.votes, q);
+    zOk = !many(mor(mand(D, g.ballot(decision != z0)), mand(CR, g.ballot(vote != z0))));
   }
-  const bool commitCoord = (g.bcast((decided ? 1 : 0) | (commit ? 2 : 0) | (ready ? 4 : 0), L.flags, coord) & 2) != 0;
-  const bool c5 = commitCoord || !g.any(ts == r4);  // (i.ts == r/4) ==> coord.commit
+  const bool c5 = mtest(C, coord) || !g.any(ts == r4);  // (i.ts == r/4) ==> coord.commit
   bool maj = false;
   if (c > 0 && zOk && c5) {
     // exists t: A = {i : i.ts >= t}, |A| > n/2, t <= r/4, all x over A equal (to the pinned value)
@@ -76,7 +72,7 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, const X0Set<W>& X0, Checks& ck, in
       const Mask<W> A = g.ballot(ts >= t);
       if (mpopc(A) > n / 2 && t <= r4) {
         const int32_t xv = g.bcast(x, L.xs, mfirst(A));
-        const bool allSame = !g.any(ts >= t && x != xv);
+        const bool allSame = !many(mand(A, g.ballot(x != xv)));
         if (allSame && (!zAny || xv == z0)) maj = true;
       }
     };
@@ -89,19 +85,15 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, const X0Set<W>& X0, Checks& ck, in
     }
   }
   const bool inv0 = keep && (noDec || maj);
-  const bool d0in = anyD && rfl32(X0.contains(d0) ? 1 : 0) != 0;
+  const bool validity = X0.all_in(g, D, decision);
+  const bool d0in = same && validity;
   const bool term = meq(D, full);
-  const bool inv1 = term && same && d0in;
-  const bool validity = !g.any(decided && !X0.contains(decision));
-  const bool integrity = !anyD || (same && d0in);
-  const bool irrev = !has_old || !g.any(old_decided && !(decided && old_decision == decision));
-  const uint32_t fb = fbit(inv0 || inv1, 0) |
-                      fbit(inv0, 1) |
-                      fbit(inv1, 2) |
-                      fbit(same, 3) |
-                      fbit(validity, 4) |
-                      fbit(integrity, 5) |
-                      fbit(irrev, 6);
+  const bool inv1 = term && d0in;
+  const bool integrity = !anyD || d0in;
+  const Mask<W> OLD = g.ballot((old_fl & F_DECIDED) != 0u);
+  const bool irrev = !has_old || !many(mandn(OLD, mand(D, g.ballot(old_decision == decision))));
+  const uint32_t fb = fbit(inv0 || inv1, 0) | fbit(inv0, 1) | fbit(inv1, 2) | fbit(same, 3) | fbit(validity, 4) |
+                      fbit(integrity, 5) | fbit(irrev, 6);
   ck.record(fb, term, c, g.lane);
 }
 
@@ -147,24 +139,25 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
     sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_LAST_VOTING);
-    // LVProcess state after init(io) (LastVoting.scala:82-109)
     X0Set<W> X0;
     X0.build(g, x0tab[grp], x0);
+    // LVProcess state after init(io) (LastVoting.scala:82-109)
     int32_t x = x0, ts = -1, vote = 0, decision = -1;
-    bool ready = false, commit = false, decided = false, halted = false;
+    uint32_t fl = g.valid ? 0u : F_HALTED;
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
     Checks ck;
     ck.reset();
-    lv_check<W>(g, L, X0, ck, 0, false, n, full, x, ts, vote, decision, decided, commit, ready, false, -1);
+    lv_check<W>(g, L, X0, ck, 0, false, n, full, x, ts, vote, decision, fl, 0u, -1);
 
     for (int k = 0; k < a.R; ++k) {
-      const bool old_decided = decided;
+      const uint32_t old_fl = fl;
       const int32_t old_decision = decision;
-      const Mask<W> act = g.ballot(!halted);
+      const Mask<W> act = g.ballot((fl & F_HALTED) == 0u);
       if (many(act)) {
         const int32_t phase = k >> 2;
         const int c = phase % n;
         const bool cAlive = mtest(act, c);
+        const uint32_t live = (fl & F_HALTED) ? 0u : 1u;
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
@@ -173,8 +166,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
           CN = g.ballot(sc.crash_round == k);
         }
         const Mask<W> HO = sc.ho(k, g.pid, good, goodS, CB, CN);
-        lv_stage<W>(g, L, x, ts, vote, decision, decided, commit, ready);
-        const int32_t cflags = g.bcast((decided ? 1 : 0) | (commit ? 2 : 0) | (ready ? 4 : 0), L.flags, c);
+        lv_stage<W>(g, L, x, ts, vote, decision);
         switch (k & 3) {
           case 0: {  // R0: send (x, ts) to coord; coord picks vote = x of maxBy ts
             const Mask<W> Mc = mand(ho_of<W>(g, L, HO, c), act);
@@ -182,11 +174,11 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
             if (cAlive && (size > n / 2 || (k == 0 && size > 0))) {
               const bool inMc = mtest(Mc, g.pid);
               const int32_t maxts = g.max32(ts, inMc);
-              const Mask<W> T = g.ballot(inMc && ts == maxts);
+              const Mask<W> T = mand(Mc, g.ballot(ts == maxts));
               const int q0 = mfirst(T);
               const int32_t xq0 = g.bcast(x, L.xs, q0);
               int win = q0;
-              const bool differ = g.any(mtest(T, g.pid) && x != xq0);
+              const bool differ = many(mand(T, g.ballot(x != xq0)));
               if (differ && a.tiebreak == PSG_TIE_CHAMP && size > 4) {
                 // CHAMP order of the coordinator's mailbox: payload depth of each
                 // candidate = longest 5-bit hash prefix shared with another entry.
@@ -203,55 +195,50 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
                 const bool inT = mtest(T, g.pid);
                 const int64_t key = (int64_t)champ_key(myh, depth);
                 const int64_t kmin = g.min64(key, inT);
-                win = mfirst(g.ballot(inT && key == kmin));
+                win = mfirst(mand(T, g.ballot(key == kmin)));
               }
               const int32_t v = g.bcast(x, L.xs, win);
               if (g.pid == c) {
                 vote = v;
-                commit = true;
+                fl |= F_COMMIT;
               }
             }
             break;
           }
           case 1: {  // R1: coord broadcasts vote if commit; receivers adopt (x, ts = r/4)
-            if (cAlive && (cflags & 2)) {
+            const bool sent = cAlive && mtest(g.ballot((fl & F_COMMIT) != 0u), c);
+            if (sent) {
               const int32_t vc = g.bcast(vote, L.votes, c);
-              if (!halted && mtest(HO, c)) {
-                x = vc;
-                ts = phase;
-              }
+              const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
+              x = rcv ? vc : x;
+              ts = rcv ? phase : ts;
             }
             break;
           }
           case 2: {  // R2: ts == r/4 send x to coord; coord ready on a majority
             const Mask<W> Mc = mand(mand(ho_of<W>(g, L, HO, c), act), g.ballot(ts == phase));
-            if (cAlive && mpopc(Mc) > need2 && g.pid == c) ready = true;
+            if (cAlive && mpopc(Mc) > need2 && g.pid == c) fl |= F_READY;
             break;
           }
           default: {  // R3: coord broadcasts vote if ready; receivers decide and exit
-            if (cAlive && (cflags & 4)) {
+            const bool sent = cAlive && mtest(g.ballot((fl & F_READY) != 0u), c);
+            if (sent) {
               const int32_t vc = g.bcast(vote, L.votes, c);
-              if (!halted && mtest(HO, c)) {
-                if (dec_round < 0) {
-                  dec_val = vc;
-                  dec_round = k;
-                }
-                decision = vc;
-                decided = true;
-                halt_round = k;
-              }
+              const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
+              const uint32_t first = rcv & (dec_round < 0 ? 1u : 0u);
+              dec_val = first ? vc : dec_val;
+              dec_round = first ? k : dec_round;
+              decision = rcv ? vc : decision;
+              halt_round = rcv ? k : halt_round;
+              fl |= rcv ? (F_DECIDED | F_HALTED) : 0u;
             }
-            if (!halted) {
-              ready = false;
-              commit = false;
-            }
-            if (halt_round == k) halted = true;
+            // ready = false; commit = false for every process that took this step
+            fl &= live ? ~(F_READY | F_COMMIT) : ~0u;
             break;
           }
         }
       }
-      lv_check<W>(g, L, X0, ck, k + 1, true, n, full, x, ts, vote, decision, decided, commit, ready, old_decided,
-                  old_decision);
+      lv_check<W>(g, L, X0, ck, k + 1, true, n, full, x, ts, vote, decision, fl, old_fl, old_decision);
     }
     finish_instance<W>(g, a, i, ck, 7, dec_val, dec_round, halt_round, x, &bc);
   }
