@@ -134,7 +134,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     dev = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(dev)
-    if world > 1:
+    launched = "WORLD_SIZE" in os.environ  # torchrun: always go through RCCL, even at world size 1
+    if launched:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
     head = run_variant(rank, world, args, args.V, args.steps, args.warmup)
     variants = {}
@@ -202,7 +203,7 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if launched:
         dist.barrier()
         dist.destroy_process_group()
 

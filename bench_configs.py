@@ -51,7 +51,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     dev = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(dev)
-    if world > 1:
+    launched = "WORLD_SIZE" in os.environ  # torchrun: always go through RCCL, even at world size 1
+    if launched:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
     results = []
     for name, alg, n, I, kw, balg in configs(args.scale):
@@ -102,7 +103,7 @@ def main():
     if rank == 0 and args.out:
         with open(args.out, "w") as f:
             json.dump(results, f, indent=1)
-    if world > 1:
+    if launched:
         dist.barrier()
         dist.destroy_process_group()
 
