@@ -34,7 +34,7 @@ def allreduce_summary(s: abi.Summary, device=None) -> abi.Summary:
     dev = device if device is not None else "cpu"
     t = torch.tensor(vals[:-1], dtype=torch.int64, device=dev)
     k = torch.tensor([vals[-1]], dtype=torch.int64, device=dev)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         dist.all_reduce(k, op=dist.ReduceOp.MAX)
     return abi.summary_from_list(t.cpu().tolist() + k.cpu().tolist())
@@ -42,6 +42,6 @@ def allreduce_summary(s: abi.Summary, device=None) -> abi.Summary:
 
 def allreduce_max(x: float, device=None) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device if device is not None else "cpu")
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
