@@ -50,7 +50,7 @@ def parse():
 
 
 def pmc_traffic_bytes(args):
-    """HBM bytes per launch of otr_kernel<1> from the newest committed PMC summary
+    """HBM bytes per launch of otr_kernel<1, false> from the newest committed PMC summary
     (profiles/*/pmc_summary.json, scripts/summarize_profile.py) of this exact workload."""
     import glob
     best = None
@@ -60,7 +60,7 @@ def pmc_traffic_bytes(args):
         except (OSError, ValueError):
             continue
         w = d.get("workload", {})
-        if ("otr_kernel<1>" in d.get("kernel", "") and "hbm" in d and w.get("n") == args.n
+        if ("otr_kernel<1" in d.get("kernel", "") and "hbm" in d and w.get("n") == args.n
                 and w.get("rounds") == args.rounds and w.get("instances_per_gpu") == args.instances
                 and w.get("value_range") == args.V):
             best = (d["hbm"]["traffic_bytes"], os.path.relpath(f, ROOT))
@@ -182,7 +182,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": "psg::otr_kernel<1>",
+                "kernel": "psg::otr_kernel<1, false>",
                 "kernel_ms": head["kernel_s"] * 1e3,
                 "bytes_per_process_round": B_ALG_OTR,
             },

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PSG_ABI_VERSION 1u
+#define PSG_ABI_VERSION 2u
 
 /* Algorithms, keyed on the reference class names. */
 enum psg_alg {
@@ -52,7 +52,11 @@ enum psg_alg {
   PSG_ALG_LAST_VOTING = 2, /* example.LastVoting     example/LastVoting.scala:11-212 */
   PSG_ALG_FLOODMIN = 3,    /* example.FloodMin       example/FloodMin.scala:8-48 */
   PSG_ALG_KSET = 4,        /* example.KSetAgreement  example/KSetAgreement.scala:21-87 */
-  PSG_ALG_BENOR = 5        /* example.BenOr          example/BenOr.scala:11-124 */
+  PSG_ALG_BENOR = 5,       /* example.BenOr          example/BenOr.scala:11-124 */
+  /* second wave */
+  PSG_ALG_OTR2 = 6,        /* example.OTR2               example/Otr2.scala:9-104 */
+  PSG_ALG_SLV = 7,         /* example.ShortLastVoting    example/ShortLastVoting.scala:13-119 */
+  PSG_ALG_KSET_ES = 8      /* example.KSetEarlyStopping  example/KSetEarlyStopping.scala:9-57 */
 };
 
 /* Which element of a Scala immutable.Map is "first" (LastVoting maxBy ties,
@@ -99,13 +103,15 @@ typedef struct psg_config {
   int32_t rounds;       /* R rounds executed per instance, 1..PSG_MAX_ROUNDS */
   uint64_t seed;
   int32_t value_range;  /* synthetic init values uniform in {1..value_range} (BenOr: {false,true}) */
-  int32_t param;        /* OTR afterDecision (Otr.scala:89, default 2); FloodMin f (FloodMin.scala:27);
-                           KSet k (KSetAgreement.scala:56); LastVoting/BenOr: unused */
+  int32_t param;        /* OTR/OTR2 afterDecision (Otr.scala:89, default 2); FloodMin f (FloodMin.scala:27);
+                           KSet k (KSetAgreement.scala:56); KSetEarlyStopping t; others unused */
   int32_t tiebreak;     /* enum psg_tiebreak */
   int32_t device;       /* HIP device ordinal */
   int32_t variant;      /* 0 = reference algorithm; 1 = test mutation */
   uint64_t batch_capacity; /* max instances per psg_run_batch call (device buffers sized for it) */
   psg_schedule sched;
+  int32_t param2;       /* KSetEarlyStopping k (KSetEarlyStopping.scala:9; param = t) */
+  int32_t reserved;
 } psg_config;
 
 /* Aggregate result of one batch. All fields are sums over instances (so a
@@ -183,6 +189,13 @@ void psg_destroy(psg_ctx* ctx);
 
 /* Library-level error text when psg_create itself fails (ctx unavailable). */
 const char* psg_create_error(void);
+
+/* Self-test hook (tests only, no reference counterpart): for each of `count` pid
+ * sets given as 64-bit masks (pids < 64), the first pid in Scala Map iteration
+ * order (enum psg_tiebreak), computed on device `device` by the helper that
+ * resolves a per-receiver `mailbox.head` (ShortLastVoting.scala:87). -1 for an
+ * empty set. */
+int psg_selftest_map_head(int32_t device, const uint64_t* sets, int32_t count, int32_t tiebreak, int32_t* out_first);
 
 #ifdef __cplusplus
 }

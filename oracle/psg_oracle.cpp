@@ -11,9 +11,11 @@
  *     psync/Round.scala:102-124 (broadcast includes self; self send bypasses the network),
  *     psync/runtime/InstanceHandler.scala:164-258 (send -> receive* -> update, exit);
  *   - algorithms: example/Otr.scala:13-86, example/LastVoting.scala:80-212,
- *     example/FloodMin.scala:8-36, example/KSetAgreement.scala:21-68, example/BenOr.scala:11-84;
+ *     example/FloodMin.scala:8-36, example/KSetAgreement.scala:21-68, example/BenOr.scala:11-84,
+ *     example/Otr2.scala:9-66, example/ShortLastVoting.scala:13-105,
+ *     example/KSetEarlyStopping.scala:9-44;
  *   - Spec: psync/Specs.scala:8-27 and the per-algorithm specs (Otr.scala:95-120,
- *     LastVoting.scala:19-70, BenOr.scala:91-115), evaluated two independent ways:
+ *     LastVoting.scala:19-70, BenOr.scala:91-115, Otr2.scala:71-96), evaluated two independent ways:
  *     (a) a Formula-tree interpreter mirroring psync/formula/Formula.scala
  *         (ForAll/Exists/Comprehension/Cardinality, lowering as in
  *         psync/macros/FormulaExtractor.scala:222-233, 297-316, 500-506);
@@ -433,6 +435,33 @@ static SpecDef otr_spec() {
   return s;
 }
 
+/* example/Otr2.scala:71-96. decision is an Option[Int]: field F_DECISION holds
+ * the value or NONE, so isDefined / get / Option equality are literal. */
+static SpecDef otr2_spec() {
+  SpecDef s;
+  Fm i = bv(0), j = bv(1), v = bv(2), ii = bv(3);
+  Fm twoThirds = div_(times(lit(2), nvar()), lit(3));
+  Fm dec = fld(F_DECISION, i);
+  Fm A = filterP(3, eq(fld(F_X, ii), v));
+  Fm allDecV = forallP(0, imp(isdef(dec), eq(get(dec), v)));
+  Fm inv0 = or_(forallP(0, not_(not_(isdef(dec)))), /* P.forall(i => !i.decision.isEmpty) */
+                existsVInt(2, and_(gt(card(A), twoThirds), allDecV)));
+  Fm inv1 = existsVInt(2, and_(eq(card(A), nvar()), allDecV));
+  Fm inv2 = existsVInt(2, allDecV);
+  s.invariants = {inv0, inv1, inv2};
+  s.termination = forallP(0, isdef(dec));
+  Fm decj = fld(F_DECISION, j);
+  s.properties.push_back({"Agreement",
+      forallP(0, forallP(1, imp(and_(isdef(dec), isdef(decj)), eq(dec, decj))))});
+  s.properties.push_back({"Validity",
+      forallP(0, imp(isdef(dec), existsP(1, eq(fld(F_X, j, T_INIT), get(dec)))))});
+  s.properties.push_back({"Integrity",
+      existsP(1, forallP(0, imp(isdef(dec), eq(get(dec), fld(F_X, j, T_INIT)))))});
+  Fm odec = fld(F_DECISION, i, T_OLD);
+  s.properties.push_back({"Irrevocability", forallP(0, imp(isdef(odec), eq(odec, dec)))});
+  return s;
+}
+
 /* example/LastVoting.scala:147-198 */
 static SpecDef lv_spec() {
   SpecDef s;
@@ -500,6 +529,9 @@ static int n_checks_of(int alg) {
     case PSG_ALG_BENOR: return 5;
     case PSG_ALG_FLOODMIN: return 2;
     case PSG_ALG_KSET: return 2;
+    case PSG_ALG_OTR2: return 8;
+    case PSG_ALG_SLV: return 2;
+    case PSG_ALG_KSET_ES: return 2;
   }
   return 0;
 }
@@ -826,12 +858,135 @@ struct BenOr {
   int32_t main_x(const P& s) const { return s.x ? 1 : 0; }
 };
 
+/* ---------------- OTR2: example/Otr2.scala:9-66 ----------------
+ * Same round as OTR (Otr2.scala:26-61: mmor, > 2n/3 adopt / decide, callback
+ * only while decision.isEmpty, decision = Some(v), after countdown); the
+ * difference is decision: Option[Int], which the Spec sees as value-or-None. */
+struct Otr2 : Otr {
+  void fields(const P& s, int64_t* f) const {
+    f[F_X] = s.x; f[F_DECIDED] = s.decided; f[F_DECISION] = s.decided ? (int64_t)s.decision : NONE;
+  }
+};
+
+/* ---------------- ShortLastVoting: example/ShortLastVoting.scala:13-105 ---------------- */
+struct SLV {
+  struct P {
+    int32_t x = 0, ts = -1;
+    bool commit = false;
+    int32_t vote = 0, decision = -1;
+    bool decided = false;
+  };
+  struct Payload { int32_t x; int32_t ts; };
+  int n, variant, tiebreak;
+  static const int L = 3;
+  int coord(int k) const { return (k / 4) % n; } /* coord(r/4), ShortLastVoting.scala:23, 37 (r/4 literal) */
+  void init(P& s, int32_t v) { /* ShortLastVoting.scala:25-31 */
+    s.x = v; s.ts = -1; s.decided = false; s.commit = false;
+  }
+  bool sends_to(const P& s, int self, int k, int dst) const {
+    switch (k % 3) {
+      case 0: return dst == coord(k);              /* Map(coord(r/4) -> (x, ts)) */
+      case 1: return self == coord(k) && s.commit; /* broadcast(vote) if coord && commit */
+      default: return s.ts == k / 4;               /* broadcast(x) if ts == r/4 */
+    }
+  }
+  Payload payload(const P& s, int, int k, int) const {
+    switch (k % 3) {
+      case 0: return {s.x, s.ts};
+      case 1: return {s.vote, 0};
+      default: return {s.x, 0};
+    }
+  }
+  static int first_in_map_order(const std::vector<Msg<Payload>>& mb, int tiebreak) {
+    std::vector<int> ins;
+    for (auto& m : mb) ins.push_back(m.src);
+    return scala_map_order(ins, tiebreak)[0];
+  }
+  bool update(P& s, int self, int k, const std::vector<Msg<Payload>>& mb, Callback& cb, const Schedule&, int) {
+    const int c = coord(k);
+    switch (k % 3) {
+      case 0: { /* ShortLastVoting.scala:39-46 */
+        if (self == c && (int)mb.size() > n / 2) {
+          /* vote = mailbox.maxBy(_._2._2)._2._1: first max in Map iteration order */
+          std::vector<int> ins;
+          for (auto& m : mb) ins.push_back(m.src);
+          bool first = true;
+          int32_t maxTs = 0, vote = 0;
+          for (int q : scala_map_order(ins, tiebreak))
+            for (auto& m : mb)
+              if (m.src == q && (first || m.payload.ts > maxTs)) { maxTs = m.payload.ts; vote = m.payload.x; first = false; }
+          s.vote = vote;
+          s.commit = true;
+        }
+        return false;
+      }
+      case 1: /* ShortLastVoting.scala:63-68 */
+        for (auto& m : mb) if (m.src == c) { s.x = m.payload.x; s.ts = k / 4; }
+        return false;
+      default: { /* ShortLastVoting.scala:84-97 */
+        const int need = variant == 1 ? 0 : n / 2;
+        if ((int)mb.size() > need) {
+          const int h = first_in_map_order(mb, tiebreak); /* mailbox.head._2 */
+          int32_t v = 0;
+          for (auto& m : mb) if (m.src == h) v = m.payload.x;
+          if (!s.decided) {
+            cb.decide(v, k);
+            s.decision = v;
+            s.decided = true;
+          }
+        }
+        s.commit = false;
+        return s.decided;
+      }
+    }
+  }
+  void fields(const P& s, int64_t* f) const {
+    f[F_X] = s.x; f[F_DECIDED] = s.decided; f[F_DECISION] = s.decision; f[F_TS] = s.ts;
+    f[F_COMMIT] = s.commit; f[F_VOTE] = s.vote;
+  }
+  int32_t main_x(const P& s) const { return s.x; }
+};
+
+/* ---------------- KSetEarlyStopping: example/KSetEarlyStopping.scala:9-44 ---------------- */
+struct KSetES {
+  struct P { int32_t est = 0; bool canDecide = false; int32_t lastNb = 0; bool decided = false; int32_t decision = 0; };
+  struct Payload { int32_t est; bool canDecide; };
+  int n, t, k, variant;
+  static const int L = 1;
+  void init(P& s, int32_t v) { s.canDecide = false; s.lastNb = n; s.est = v; } /* :16-21 */
+  bool sends_to(const P&, int, int, int) const { return true; }                   /* broadcast((est, canDecide)) */
+  Payload payload(const P& s, int, int, int) const { return {s.est, s.canDecide}; }
+  bool update(P& s, int, int r, const std::vector<Msg<Payload>>& mb, Callback& cb, const Schedule&, int) {
+    const int currNb = (int)mb.size(); /* :31-41 */
+    if (r > t / k || s.canDecide) {
+      cb.decide(s.est, r);
+      s.decided = true; s.decision = s.est;
+      return true;
+    }
+    /* est = mailbox.map(_._2._1).min. An empty mailbox (pure HO mode only: with
+     * the self bit a running process always hears itself) would throw in Scala;
+     * here est is left unchanged. */
+    bool ex = false;
+    for (auto& m : mb) ex = ex || m.payload.canDecide; /* mailbox.exists(_._2._2) */
+    if (!mb.empty()) {
+      int32_t mn = INT32_MAX;
+      for (auto& m : mb) mn = std::min(mn, m.payload.est);
+      s.est = mn;
+    }
+    s.canDecide = variant == 1 ? true : (ex || s.lastNb - currNb < k);
+    s.lastNb = currNb;
+    return false;
+  }
+  void fields(const P& s, int64_t* fv) const { fv[F_X] = s.est; fv[F_DECIDED] = s.decided; fv[F_DECISION] = s.decision; }
+  int32_t main_x(const P& s) const { return s.est; }
+};
+
 /* ------------------------------------------------------------------ */
 /* Hand-lowered Spec evaluator (what the GPU kernel implements)         */
 /* ------------------------------------------------------------------ */
 struct Direct {
   /* inputs */
-  int n, alg, kparam;
+  int n, alg, kparam, kparam2;
   int64_t r;
   const std::vector<int64_t>* cur;  /* [F][p] */
   const std::vector<int64_t>* old;
@@ -948,10 +1103,32 @@ struct Direct {
       bool pred = true;
       for (int p = 0; p < n; ++p) if (!(cur[F_HOSIZE][p] > n / 2)) pred = false;
       ck = {inv0, inv0, same, irrevocability(), pred};
-    } else { /* FloodMin / KSet: build-defined k-agreement (KSetAgreement.scala:144) */
-      int k = alg == PSG_ALG_FLOODMIN ? 1 : kparam;
+    } else if (alg == PSG_ALG_OTR2) {
+      /* Otr2.scala:75-87: no keepInit; inv0's first disjunct is "all decided" */
+      int thr = 2 * n / 3;
+      bool e0 = false, e1 = false;
+      std::set<int64_t> xs;
+      for (int p = 0; p < n; ++p) xs.insert(cur[F_X][p]);
+      for (int64_t v : xs) {
+        int cnt = 0;
+        for (int p = 0; p < n; ++p) if (cur[F_X][p] == v) ++cnt;
+        bool condv = !any || (same && v == d0);
+        if (cnt > thr && condv) e0 = true;
+        if (cnt == n && condv) e1 = true;
+      }
+      bool inv0 = term || e0, inv1 = e1, inv2 = same;
+      bool d0in = any && inX0(d0);
+      ck = {inv0 || inv1 || inv2, inv0, inv1, inv2, same, validity(), !any || (same && d0in), irrevocability()};
+    } else {
+      /* TrivialSpec algorithms: build-defined k-agreement + validity
+       * (KSetAgreement.scala:144). FloodMin / KSet / KSetEarlyStopping (crash-stop
+       * algorithms): over never-crashed deciders; ShortLastVoting (HO model,
+       * consensus): uniform, over every decider. */
+      int k = alg == PSG_ALG_KSET ? kparam : alg == PSG_ALG_KSET_ES ? kparam2 : 1;
+      bool uniform = alg == PSG_ALG_SLV;
       std::set<int64_t> Y;
-      for (int p = 0; p < n; ++p) if (cur[F_DECIDED][p] && !(*crashed)[p]) Y.insert(cur[F_DECISION][p]);
+      for (int p = 0; p < n; ++p)
+        if (cur[F_DECIDED][p] && (uniform || !(*crashed)[p])) Y.insert(cur[F_DECISION][p]);
       ck = {(int)Y.size() <= k, validity()};
     }
   }
@@ -1005,8 +1182,10 @@ static void run_engine(Alg& alg, const psg_config& cfg, uint64_t inst, const int
     for (int p = 0; p < n; ++p) st[p].t = {{p, x0[p]}};
 
   SpecDef sd;
-  bool has_spec = cfg.alg == PSG_ALG_OTR || cfg.alg == PSG_ALG_LAST_VOTING || cfg.alg == PSG_ALG_BENOR;
+  bool has_spec = cfg.alg == PSG_ALG_OTR || cfg.alg == PSG_ALG_LAST_VOTING || cfg.alg == PSG_ALG_BENOR ||
+                  cfg.alg == PSG_ALG_OTR2;
   if (cfg.alg == PSG_ALG_OTR) sd = otr_spec();
+  if (cfg.alg == PSG_ALG_OTR2) sd = otr2_spec();
   if (cfg.alg == PSG_ALG_LAST_VOTING) sd = lv_spec();
   if (cfg.alg == PSG_ALG_BENOR) sd = benor_spec();
   if (spec_mode != SPEC_DIRECT && !has_spec) spec_mode = SPEC_DIRECT;
@@ -1038,7 +1217,7 @@ static void run_engine(Alg& alg, const psg_config& cfg, uint64_t inst, const int
     snapshot(fcur);
     std::vector<bool> ck, ck2;
     bool term = false, term2 = false;
-    Direct d{n, cfg.alg, cfg.param, c, fcur, fold, finit, &crashed, has_old};
+    Direct d{n, cfg.alg, cfg.param, cfg.param2, c, fcur, fold, finit, &crashed, has_old};
     if (spec_mode != SPEC_INTERP) d.eval(ck, term);
     if (spec_mode != SPEC_DIRECT) {
       SpecState ss;
@@ -1122,7 +1301,8 @@ static int validate(const psg_config* c, std::string& err) {
   if (!c) { err = "null config"; return PSG_EINVAL; }
   if (c->n < 1 || c->n > PSG_MAX_N) { err = "n out of range"; return PSG_EINVAL; }
   if (c->rounds < 1 || c->rounds > PSG_MAX_ROUNDS) { err = "rounds out of range"; return PSG_EINVAL; }
-  if (c->alg < PSG_ALG_OTR || c->alg > PSG_ALG_BENOR) { err = "unknown alg"; return PSG_EINVAL; }
+  if (c->alg < PSG_ALG_OTR || c->alg > PSG_ALG_KSET_ES) { err = "unknown alg"; return PSG_EINVAL; }
+  if (c->alg == PSG_ALG_KSET_ES && (c->param < 0 || c->param2 < 1)) { err = "KSetEarlyStopping needs t >= 0, k >= 1"; return PSG_EINVAL; }
   if (c->alg != PSG_ALG_BENOR && c->value_range < 1) { err = "value_range < 1"; return PSG_EINVAL; }
   return 0;
 }
@@ -1135,6 +1315,9 @@ static void run_one(const psg_config& cfg, uint64_t inst, const int32_t* init, i
     case PSG_ALG_FLOODMIN: { FloodMin a{cfg.n, cfg.param, cfg.variant}; run_engine(a, cfg, inst, init, spec_mode, eho, out, trace); break; }
     case PSG_ALG_KSET: { KSet a{cfg.n, cfg.param, cfg.variant, cfg.tiebreak}; run_engine(a, cfg, inst, init, spec_mode, eho, out, trace); break; }
     case PSG_ALG_BENOR: { BenOr a{cfg.n, cfg.variant}; run_engine(a, cfg, inst, init, spec_mode, eho, out, trace); break; }
+    case PSG_ALG_OTR2: { Otr2 a; a.n = cfg.n; a.afterDecision = cfg.param; a.variant = cfg.variant; run_engine(a, cfg, inst, init, spec_mode, eho, out, trace); break; }
+    case PSG_ALG_SLV: { SLV a{cfg.n, cfg.variant, cfg.tiebreak}; run_engine(a, cfg, inst, init, spec_mode, eho, out, trace); break; }
+    case PSG_ALG_KSET_ES: { KSetES a{cfg.n, cfg.param, cfg.param2, cfg.variant}; run_engine(a, cfg, inst, init, spec_mode, eho, out, trace); break; }
   }
 }
 

@@ -5,13 +5,16 @@ binding (oracle/oracle.py): both libraries speak the same C structs.
 """
 import ctypes as C
 
-PSG_ABI_VERSION = 1
+PSG_ABI_VERSION = 2
 
 PSG_ALG_OTR = 1
 PSG_ALG_LAST_VOTING = 2
 PSG_ALG_FLOODMIN = 3
 PSG_ALG_KSET = 4
 PSG_ALG_BENOR = 5
+PSG_ALG_OTR2 = 6
+PSG_ALG_SLV = 7
+PSG_ALG_KSET_ES = 8
 
 PSG_TIE_CHAMP = 0
 PSG_TIE_MIN_PID = 1
@@ -36,6 +39,9 @@ CLASS_TO_ALG = {
     "example.FloodMin": PSG_ALG_FLOODMIN,
     "example.KSetAgreement": PSG_ALG_KSET,
     "example.BenOr": PSG_ALG_BENOR,
+    "example.OTR2": PSG_ALG_OTR2,
+    "example.ShortLastVoting": PSG_ALG_SLV,
+    "example.KSetEarlyStopping": PSG_ALG_KSET_ES,
 }
 
 # Check-slot names per algorithm (psg_check_name). Slot 0 of OTR/LV/BenOr is
@@ -48,6 +54,10 @@ CHECK_NAMES = {
     PSG_ALG_BENOR: ["Safety", "Invariant0", "Agreement", "Irrevocability", "SafetyPredicate"],
     PSG_ALG_FLOODMIN: ["KAgreement", "KValidity"],
     PSG_ALG_KSET: ["KAgreement", "KValidity"],
+    PSG_ALG_OTR2: ["Safety", "Invariant0", "Invariant1", "Invariant2",
+                   "Agreement", "Validity", "Integrity", "Irrevocability"],
+    PSG_ALG_SLV: ["KAgreement", "KValidity"],
+    PSG_ALG_KSET_ES: ["KAgreement", "KValidity"],
 }
 # Slots whose falsity is a violation (invariant slots are informational: an
 # individual invariant of a sequence legitimately fails before/after its phase;
@@ -59,6 +69,9 @@ VIOLATION_SLOTS = {
     PSG_ALG_BENOR: [0, 2, 3],
     PSG_ALG_FLOODMIN: [0, 1],
     PSG_ALG_KSET: [0, 1],
+    PSG_ALG_OTR2: [0, 4, 5, 6, 7],
+    PSG_ALG_SLV: [0, 1],
+    PSG_ALG_KSET_ES: [0, 1],
 }
 
 
@@ -87,6 +100,8 @@ class Config(C.Structure):
         ("variant", C.c_int32),
         ("batch_capacity", C.c_uint64),
         ("sched", Schedule),
+        ("param2", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 

@@ -73,6 +73,9 @@ static int n_checks(int alg) {
     case PSG_ALG_BENOR: return 5;
     case PSG_ALG_FLOODMIN: return 2;
     case PSG_ALG_KSET: return 2;
+    case PSG_ALG_OTR2: return 8;
+    case PSG_ALG_SLV: return 2;
+    case PSG_ALG_KSET_ES: return 2;
   }
   return 0;
 }
@@ -107,6 +110,9 @@ static hipError_t launch_alg(const psg_ctx* c, const KArgs& a, int grid) {
     case PSG_ALG_FLOODMIN: return launch_floodmin(a, c->W, grid, c->stream);
     case PSG_ALG_KSET: return launch_kset(a, c->W, grid, c->stream);
     case PSG_ALG_BENOR: return launch_benor(a, c->W, grid, c->stream);
+    case PSG_ALG_OTR2: return launch_otr2(a, c->W, grid, c->stream);
+    case PSG_ALG_SLV: return launch_slv(a, c->W, grid, c->stream);
+    case PSG_ALG_KSET_ES: return launch_kset_es(a, c->W, grid, c->stream);
   }
   return hipErrorInvalidValue;
 }
@@ -118,6 +124,9 @@ static const void* kernel_ptr(int alg, int W) {
     case PSG_ALG_FLOODMIN: return floodmin_kernel_ptr(W);
     case PSG_ALG_KSET: return kset_kernel_ptr(W);
     case PSG_ALG_BENOR: return benor_kernel_ptr(W);
+    case PSG_ALG_OTR2: return otr2_kernel_ptr(W);
+    case PSG_ALG_SLV: return slv_kernel_ptr(W);
+    case PSG_ALG_KSET_ES: return kset_es_kernel_ptr(W);
   }
   return nullptr;
 }
@@ -131,6 +140,7 @@ static KArgs make_args(const psg_ctx* c) {
   a.R = f.rounds;
   a.V = f.value_range;
   a.param = f.param;
+  a.param2 = f.param2;
   a.variant = f.variant;
   a.tiebreak = f.tiebreak;
   a.drop_log2 = f.sched.drop_log2;
@@ -225,6 +235,23 @@ int psg_config_default(psg_config* cfg, int32_t alg, int32_t n) {
       cfg->sched.good_p32 = 0;
       cfg->sched.ho_min = n / 2;
       break;
+    case PSG_ALG_OTR2: cfg->param = 2; break;  // afterDecision (Otr2.scala:69)
+    case PSG_ALG_SLV:
+      cfg->rounds = 30;
+      cfg->value_range = (1 << 15) - 1;
+      cfg->sched.drop_log2 = 4;
+      cfg->sched.good_p32 = 0;
+      cfg->sched.crash_fmax = (n - 1) / 2;
+      break;
+    case PSG_ALG_KSET_ES:  // t = 2, k = 2 (KSetEarlyStopping.scala:63-67)
+      cfg->param = 2;
+      cfg->param2 = 2;
+      cfg->rounds = 3;
+      cfg->value_range = 1000000;
+      cfg->sched.drop_log2 = 0;
+      cfg->sched.good_p32 = 0;
+      cfg->sched.crash_fmax = 2;
+      break;
     default: return PSG_EINVAL;
   }
   return PSG_OK;
@@ -235,7 +262,8 @@ int psg_check_count(int32_t alg) { return n_checks(alg); }
 const char* psg_check_name(int32_t alg, int32_t slot) {
   if (slot < 0 || slot >= n_checks(alg)) return nullptr;
   switch (alg) {
-    case PSG_ALG_OTR: return k_names_otr[slot];
+    case PSG_ALG_OTR:
+    case PSG_ALG_OTR2: return k_names_otr[slot];
     case PSG_ALG_LAST_VOTING: return k_names_lv[slot];
     case PSG_ALG_BENOR: return k_names_benor[slot];
     default: return k_names_k[slot];
@@ -247,7 +275,8 @@ int psg_alg_from_class(const char* name) {
   static const struct { const char* n; int id; } tab[] = {
       {"example.OTR", PSG_ALG_OTR}, {"example.LastVoting", PSG_ALG_LAST_VOTING},
       {"example.FloodMin", PSG_ALG_FLOODMIN}, {"example.KSetAgreement", PSG_ALG_KSET},
-      {"example.BenOr", PSG_ALG_BENOR}};
+      {"example.BenOr", PSG_ALG_BENOR}, {"example.OTR2", PSG_ALG_OTR2},
+      {"example.ShortLastVoting", PSG_ALG_SLV}, {"example.KSetEarlyStopping", PSG_ALG_KSET_ES}};
   for (auto& t : tab)
     if (std::strcmp(t.n, name) == 0) return t.id;
   return PSG_EINVAL;
@@ -255,16 +284,46 @@ int psg_alg_from_class(const char* name) {
 
 const char* psg_create_error(void) { return g_create_err.c_str(); }
 
+int psg_selftest_map_head(int32_t device, const uint64_t* sets, int32_t count, int32_t tiebreak, int32_t* out_first) {
+  if (!sets || !out_first || count < 0) return PSG_EINVAL;
+  if (tiebreak != PSG_TIE_CHAMP && tiebreak != PSG_TIE_MIN_PID) return PSG_EINVAL;
+  if (count == 0) return PSG_OK;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return PSG_ENODEV;
+  if (hipSetDevice(device) != hipSuccess) return PSG_ENODEV;
+  uint64_t* d_sets = nullptr;
+  int32_t* d_out = nullptr;
+  int rc = PSG_OK;
+  if (hipMalloc(&d_sets, sizeof(uint64_t) * count) != hipSuccess ||
+      hipMalloc(&d_out, sizeof(int32_t) * count) != hipSuccess) {
+    rc = PSG_ENOMEM;
+  } else if (hipMemcpy(d_sets, sets, sizeof(uint64_t) * count, hipMemcpyHostToDevice) != hipSuccess ||
+             launch_champ_selftest(d_sets, count, tiebreak, d_out, nullptr) != hipSuccess ||
+             hipMemcpy(out_first, d_out, sizeof(int32_t) * count, hipMemcpyDeviceToHost) != hipSuccess) {
+    rc = PSG_EIO;
+  }
+  if (d_sets) (void)hipFree(d_sets);
+  if (d_out) (void)hipFree(d_out);
+  return rc;
+}
+
 static int validate(const psg_config* cfg, std::string& m) {
   if (!cfg) { m = "null config"; return PSG_EINVAL; }
   if (cfg->abi_version != PSG_ABI_VERSION) { m = "ABI version mismatch"; return PSG_EINVAL; }
-  if (cfg->alg < PSG_ALG_OTR || cfg->alg > PSG_ALG_BENOR) { m = "unknown algorithm"; return PSG_EINVAL; }
+  if (cfg->alg < PSG_ALG_OTR || cfg->alg > PSG_ALG_KSET_ES) { m = "unknown algorithm"; return PSG_EINVAL; }
   if (cfg->n < 1 || cfg->n > PSG_MAX_N) { m = "n out of range 1..256"; return PSG_EINVAL; }
   if (cfg->rounds < 1 || cfg->rounds > PSG_MAX_ROUNDS) { m = "rounds out of range 1..250"; return PSG_EINVAL; }
   if (cfg->alg != PSG_ALG_BENOR && cfg->value_range < 1) { m = "value_range must be >= 1"; return PSG_EINVAL; }
   if (cfg->alg == PSG_ALG_KSET && cfg->param < 1) { m = "KSetAgreement needs k >= 1"; return PSG_EINVAL; }
   if (cfg->alg == PSG_ALG_FLOODMIN && cfg->param < 0) { m = "FloodMin needs f >= 0"; return PSG_EINVAL; }
-  if (cfg->alg == PSG_ALG_OTR && cfg->param < 1) { m = "OTR needs afterDecision >= 1"; return PSG_EINVAL; }
+  if ((cfg->alg == PSG_ALG_OTR || cfg->alg == PSG_ALG_OTR2) && cfg->param < 1) {
+    m = "OTR needs afterDecision >= 1";
+    return PSG_EINVAL;
+  }
+  if (cfg->alg == PSG_ALG_KSET_ES && (cfg->param < 0 || cfg->param2 < 1)) {
+    m = "KSetEarlyStopping needs t >= 0 and k >= 1";
+    return PSG_EINVAL;
+  }
   if (cfg->tiebreak != PSG_TIE_CHAMP && cfg->tiebreak != PSG_TIE_MIN_PID) { m = "bad tiebreak"; return PSG_EINVAL; }
   if (cfg->sched.drop_log2 > 16) { m = "drop_log2 > 16"; return PSG_EINVAL; }
   if (cfg->batch_capacity < 1) { m = "batch_capacity must be >= 1"; return PSG_EINVAL; }

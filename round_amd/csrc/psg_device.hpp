@@ -29,7 +29,7 @@ struct KArgs {
   psg_process_record* out_rec;       // nullable: [count][n]
   unsigned long long* counters;      // [NCOUNTERS]
   uint64_t seed;
-  int32_t n, R, V, param, variant, tiebreak;
+  int32_t n, R, V, param, param2, variant, tiebreak;
   uint32_t drop_log2, good_p32;
   int32_t good_min, crash_fmax, ho_min;
   uint32_t self_bit;
@@ -138,6 +138,7 @@ PSG_DEV int champ_cpl(uint32_t a, uint32_t b) {  // shared leading fragments, a 
   int t = __builtin_ctz(a ^ b);
   return t / 5;
 }
+
 
 // ---------------------------------------------------------------- digest
 PSG_DEV uint64_t splitmix64(uint64_t x) {
@@ -293,6 +294,51 @@ PSG_DEV uint64_t readlane64(uint64_t v, int q) {
 // ---------------------------------------------------------------- group of W waves = one instance
 // LDS per group (W > 1): ballot ping-pong [2][W] + reduction scratch [W] + staged
 // per-process arrays. For W == 1 everything stays in registers (readlane).
+// First element of a pid set in Scala Map iteration order, for a per-lane set
+// (every receiver has its own mailbox). CHAMP pre-order: at each trie level the
+// payload entries (fragments holding exactly one element) come first in
+// ascending fragment order, then the sub-nodes; so the head is the payload with
+// the smallest fragment at the first level that has one, after descending into
+// the smallest multi-element fragment. ChampTable holds, per level l and
+// fragment f, the mask of pids whose improve(pid) has fragment f at level l.
+template <int W>
+struct ChampTable {
+  uint64_t b[7][32][W];
+  // once per block
+  PSG_DEV void build(int n) {
+    for (int e = threadIdx.x; e < 7 * 32 * W; e += blockDim.x) {
+      const int l = e / (32 * W), f = (e / W) % 32, w = e % W;
+      uint64_t m = 0;
+      for (int j = 0; j < 64; ++j) {
+        const int q = w * 64 + j;
+        if (q < n && ((scala_improve((uint32_t)q) >> (5 * l)) & 31u) == (uint32_t)f) m |= 1ull << j;
+      }
+      b[l][f][w] = m;
+    }
+  }
+};
+
+template <int W>
+PSG_DEV int champ_first(const ChampTable<W>& T, Mask<W> cur, int tiebreak) {
+  const int m = mpopc(cur);
+  if (m == 0) return -1;
+  if (tiebreak == PSG_TIE_MIN_PID || m <= 4) return mfirst(cur);  // Map1..Map4: insertion order
+  for (int l = 0; l < 7; ++l) {
+    int sub = -1;
+    for (int f = 0; f < 32; ++f) {
+      Mask<W> e;
+#pragma unroll
+      for (int w = 0; w < W; ++w) e.w[w] = cur.w[w] & T.b[l][f][w];
+      const int pc = mpopc(e);
+      if (pc == 1) return mfirst(e);
+      if (pc >= 2 && sub < 0) sub = f;
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) cur.w[w] &= T.b[l][sub][w];
+  }
+  return mfirst(cur);  // unreachable: hashes of distinct pids differ
+}
+
 template <int W>
 struct Grp {
   int lane;   // 0..63
@@ -330,6 +376,13 @@ struct Grp {
   PSG_DEV int32_t bcast(int32_t mine, const int32_t* staged, int q) const {
     if constexpr (W == 1) return readlane32(mine, q);
     else return rfl32(staged[q]);
+  }
+
+  // value of process q for a per-lane q (call from converged code): W==1 a
+  // ds_bpermute of `mine`; W>1 from a staged LDS array.
+  PSG_DEV int32_t gather(int32_t mine, const int32_t* staged, int q) const {
+    if constexpr (W == 1) return __shfl(mine, q);
+    else return staged[q];
   }
 
   // group reductions over valid lanes (inactive lanes contribute the identity)
@@ -812,6 +865,41 @@ PSG_DEV int32_t majority_candidate(Grp<W>& g, int32_t x) {
 
 // Shared by FloodMin and KSet: slot 0 KAgreement (|{decisions of correct
 // deciders}| <= k), slot 1 KValidity (every decision is an initial value).
+// vote = mailbox.maxBy(_._2._2)._2._1 over a uniform mailbox Mc of (x, ts)
+// messages (LastVoting.scala:132, ShortLastVoting.scala:43): the first maximal ts
+// in Scala Map iteration order — insertion order (ascending pid) up to 4 entries,
+// CHAMP order beyond, from per-lane CHAMP sort keys and a min-reduction. Only
+// needed when the maximal-ts senders disagree on x.
+template <int W>
+PSG_DEV int32_t maxby_ts_x(Grp<W>& g, const int32_t* xs, const Mask<W>& Mc, int size, int32_t x, int32_t ts,
+                           uint32_t myh, int tiebreak) {
+  const bool inMc = mtest(Mc, g.pid);
+  const int32_t maxts = g.max32(ts, inMc);
+  const Mask<W> T = mand(Mc, g.ballot(ts == maxts));
+  const int q0 = mfirst(T);
+  const int32_t xq0 = g.bcast(x, xs, q0);
+  int win = q0;
+  const bool differ = many(mand(T, g.ballot(x != xq0)));
+  if (differ && tiebreak == PSG_TIE_CHAMP && size > 4) {
+    // payload depth of each candidate = longest 5-bit hash prefix shared with another entry
+    int depth = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint64_t m = Mc.w[w];
+      while (m) {
+        const int f = w * 64 + __builtin_ctzll(m);
+        m &= m - 1;
+        if (f != g.pid) depth = max(depth, champ_cpl(myh, scala_improve((uint32_t)f)));
+      }
+    }
+    const bool inT = mtest(T, g.pid);
+    const int64_t key = (int64_t)champ_key(myh, depth);
+    const int64_t kmin = g.min64(key, inT);
+    win = mfirst(mand(T, g.ballot(key == kmin)));
+  }
+  return g.bcast(x, xs, win);
+}
+
 template <int W>
 PSG_DEV void kagree_check(Grp<W>& g, Checks& ck, int c, int kk, const Mask<W>& full, bool decided, int32_t decision,
                           const X0Set<W>& X0, bool crashed, const int32_t* dstaged) {

@@ -1,0 +1,142 @@
+// psg_kset_es.hip — early-stopping k-set agreement on gfx950.
+//
+// Reference: example/KSetEarlyStopping.scala:9-44 (KSetESProcess). One round,
+// broadcast (est, canDecide); a process decides est and exits once r > t/k or
+// canDecide, otherwise est = min of the received estimates and
+// canDecide = (some sender could decide) || lastNb - |mailbox| < k.
+// est = mailbox.map(_._2._1).min visits the distinct sender estimates in
+// ascending order (group min-reduction) and resolves each receiver at the first
+// value whose sender set meets its mailbox; with the self bit a receiver also
+// stops at its own estimate. Spec: TrivialSpec; the build checks k-agreement over
+// never-crashed deciders and validity, like KSetAgreement.
+#include "psg_device.hpp"
+#include "psg_kernels.hpp"
+
+namespace psg {
+
+template <int W>
+struct EsLds {
+  int32_t ds[W > 1 ? 64 * W : 1];
+};
+
+template <int W>
+__global__ void __launch_bounds__(Geometry<W>::kThreads) kset_es_kernel(KArgs a) {
+  __shared__ BlockCounters bc;
+  __shared__ uint64_t xb[2 * W];
+  __shared__ int64_t red[2 * W];
+  __shared__ EsLds<W> L;
+  __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
+  counters_init(&bc);
+  __syncthreads();
+  Grp<W> g;
+  grp_setup(g, a, xb, red);
+  constexpr int G = Geometry<W>::kGroups;
+  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int n = a.n;
+  const int t = a.param, kk = a.param2;
+  const Mask<W> full = mfull<W>(n);
+
+  for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
+    const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
+    Sched<W> sc;
+    sc.setup(a, inst, g.pid, g.valid);
+    sc.prep_good(0, g.lane, a.R);
+    const bool crashed = sc.crash_round >= 0;
+    int32_t x0 = 0;
+    if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_KSET_ES);
+    X0Set<W> X0;
+    X0.build(g, x0tab[grp], x0);
+    // KSetESProcess state after init(io) (KSetEarlyStopping.scala:16-21)
+    int32_t est = x0, lastNb = n, decision = 0;
+    bool cd = false, decided = false, halted = !g.valid;
+    int32_t dec_val = 0, dec_round = -1, halt_round = -1;
+    Checks ck;
+    ck.reset();
+    auto check = [&](int c) {
+      if constexpr (W > 1) {
+        L.ds[g.pid] = decision;
+        __syncthreads();
+      }
+      kagree_check<W>(g, ck, c, kk, full, decided, decision, X0, crashed, L.ds);
+    };
+    check(0);
+    for (int k = 0; k < a.R; ++k) {
+      const Mask<W> act = g.ballot(!halted);
+      if (many(act)) {
+        Mask<W> goodS;
+        const bool good = sc.good_round(k, g.lane, a.R, goodS);
+        Mask<W> CB = mzero<W>(), CN = mzero<W>();
+        if (sc.crash_on) {
+          CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
+          CN = g.ballot(sc.crash_round == k);
+        }
+        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+        const int currNb = mpopc(M);
+        const bool anyCD = many(mand(M, g.ballot(cd)));  // mailbox.exists(_._2._2), pre-update flags
+        const bool decideNow = !halted && (k > t / kk || cd);
+        // est = min over the mailbox's estimates (unchanged if the mailbox is empty)
+        bool unres = !halted && !decideNow && currNb > 0;
+        const bool selfIn = mtest(M, g.pid);
+        int32_t nest = est;
+        Mask<W> rem = act;
+        while (many(rem) && g.any(unres)) {
+          const int32_t v = g.min32(est, mtest(rem, g.pid));
+          const Mask<W> E = mand(g.ballot(est == v), rem);
+          rem = mandn(rem, E);
+          if (unres) {
+            if (many(mand(M, E))) {
+              nest = v;
+              unres = false;
+            } else if (selfIn && v >= est) {
+              unres = false;  // nothing below the receiver's own estimate reached it
+            }
+          }
+        }
+        if (decideNow) {  // callback.decide(est); exitAtEndOfRound (KSetEarlyStopping.scala:32-34)
+          dec_val = est;
+          dec_round = k;
+          decided = true;
+          decision = est;
+          halt_round = k;
+          halted = true;
+        } else if (!halted) {  // KSetEarlyStopping.scala:36-38 (variant 1: mutation, always canDecide)
+          est = nest;
+          cd = a.variant == 1 ? true : (anyCD || lastNb - currNb < kk);
+          lastNb = currNb;
+        }
+      }
+      check(k + 1);
+    }
+    finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, est, &bc);
+  }
+  __syncthreads();
+  counters_flush(&bc, a.counters, 2, a.R);
+}
+
+template <int W>
+static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(kset_es_kernel<W>, dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_kset_es(const KArgs& a, int W, int grid, hipStream_t s) {
+  switch (W) {
+    case 1: return launch_w<1>(a, grid, s);
+    case 2: return launch_w<2>(a, grid, s);
+    case 3: return launch_w<3>(a, grid, s);
+    case 4: return launch_w<4>(a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+const void* kset_es_kernel_ptr(int W) {
+  switch (W) {
+    case 1: return (const void*)kset_es_kernel<1>;
+    case 2: return (const void*)kset_es_kernel<2>;
+    case 3: return (const void*)kset_es_kernel<3>;
+    case 4: return (const void*)kset_es_kernel<4>;
+  }
+  return nullptr;
+}
+
+}  // namespace psg

@@ -172,32 +172,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
             const Mask<W> Mc = mand(ho_of<W>(g, L, HO, c), act);
             const int size = mpopc(Mc);
             if (cAlive && (size > n / 2 || (k == 0 && size > 0))) {
-              const bool inMc = mtest(Mc, g.pid);
-              const int32_t maxts = g.max32(ts, inMc);
-              const Mask<W> T = mand(Mc, g.ballot(ts == maxts));
-              const int q0 = mfirst(T);
-              const int32_t xq0 = g.bcast(x, L.xs, q0);
-              int win = q0;
-              const bool differ = many(mand(T, g.ballot(x != xq0)));
-              if (differ && a.tiebreak == PSG_TIE_CHAMP && size > 4) {
-                // CHAMP order of the coordinator's mailbox: payload depth of each
-                // candidate = longest 5-bit hash prefix shared with another entry.
-                int depth = 0;
-#pragma unroll
-                for (int w = 0; w < W; ++w) {
-                  uint64_t m = Mc.w[w];
-                  while (m) {
-                    const int f = w * 64 + __builtin_ctzll(m);
-                    m &= m - 1;
-                    if (f != g.pid) depth = max(depth, champ_cpl(myh, scala_improve((uint32_t)f)));
-                  }
-                }
-                const bool inT = mtest(T, g.pid);
-                const int64_t key = (int64_t)champ_key(myh, depth);
-                const int64_t kmin = g.min64(key, inT);
-                win = mfirst(mand(T, g.ballot(key == kmin)));
-              }
-              const int32_t v = g.bcast(x, L.xs, win);
+              const int32_t v = maxby_ts_x<W>(g, L.xs, Mc, size, x, ts, myh, a.tiebreak);
               if (g.pid == c) {
                 vote = v;
                 fl |= F_COMMIT;

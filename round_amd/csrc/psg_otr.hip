@@ -1,6 +1,9 @@
-// psg_otr.hip — OTR (one-third rule) on gfx950.
+// psg_otr.hip — OTR (one-third rule) and OTR2 on gfx950.
 //
-// Reference: example/Otr.scala:13-128 (OtrProcess, OTR.spec).
+// Reference: example/Otr.scala:13-128 (OtrProcess, OTR.spec); example/Otr2.scala:9-104
+// (Otr2Process: the same round with decision: Option[Int]; OTR2.spec has no
+// keepInit conjunct, Invariant0's first disjunct is "everyone decided" and
+// Invariant2 is "all decisions equal").
 // One wave64 per instance, lane = process (n <= 64); W waves per instance for
 // n > 64. Per round: HO(p) from Philox, mailbox M(p) = HO(p) & alive,
 // mmor (Otr.scala:44-49) as a loop over the distinct values v of the alive
@@ -29,7 +32,7 @@ struct OtrLds {
 //   bit 3  old(i.decided) && !(i.decided && old(i.decision) == i.decision)  Irrevocability
 // V.exists(v => |{i : i.x == v}| > 2n/3 && all decisions == v): with decisions only
 // v = d0 can qualify; without, v must be a strict majority (Boyer-Moore candidate).
-template <int W>
+template <int W, bool V2>
 PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, int c, bool has_old, int n,
                        const Mask<W>& full, int32_t x, uint32_t dec01, int32_t decision, uint32_t old01,
                        int32_t old_decision, uint32_t valid01) {
@@ -41,7 +44,7 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
   const Mask<W> D = g.ballot(dec01 != 0u);
   const bool anyD = many(D);
   const int32_t d0 = anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
-  const bool keep = X0.all_in(g, full, x);                           // keepInit
+  const bool keep = V2 || X0.all_in(g, full, x);                     // keepInit (OTR only)
   const bool validity = X0.all_in(g, D, decision);                   // decisions are initial values
   const bool same = !many(mand(D, g.ballot(decision != d0)));        // Agreement
   const Mask<W> OLD = g.ballot(old01 != 0u);                         // Irrevocability
@@ -51,18 +54,19 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
   const bool condv = !anyD || same;
   const bool e0 = condv && cnt > sthr;
   const bool e1 = condv && cnt == n;
-  const bool inv0 = (!anyD || e0) && keep;
-  const bool inv1 = e1 && keep;
   const bool term = meq(D, full);
   const bool d0in = same && validity;  // all decisions equal d0 and are initial values
-  const bool inv2 = term && d0in;
+  // OTR: Otr.scala:99-110; OTR2: Otr2.scala:75-87
+  const bool inv0 = V2 ? (term || e0) : ((!anyD || e0) && keep);
+  const bool inv1 = V2 ? e1 : (e1 && keep);
+  const bool inv2 = V2 ? same : (term && d0in);
   const bool integrity = !anyD || d0in;
   const uint32_t fb = fbit(inv0 || inv1 || inv2, 0) | fbit(inv0, 1) | fbit(inv1, 2) | fbit(inv2, 3) |
                       fbit(same, 4) | fbit(validity, 5) | fbit(integrity, 6) | fbit(irrev, 7);
   ck.record(fb, term, c, g.lane);
 }
 
-template <int W>
+template <int W, bool V2>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[2 * W];
@@ -95,7 +99,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
     Checks ck;
     ck.reset();
-    otr_check<W>(g, L, X0, ck, 0, false, n, full, x, dec01, decision, 0u, -1, valid01);
+    otr_check<W, V2>(g, L, X0, ck, 0, false, n, full, x, dec01, decision, 0u, -1, valid01);
 
     for (int k = 0; k < a.R; ++k) {
       const uint32_t old01 = dec01;
@@ -146,7 +150,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
         halt_round = h ? k : halt_round;
         halted01 |= h;
       }
-      otr_check<W>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, old01, old_decision, valid01);
+      otr_check<W, V2>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, old01, old_decision, valid01);
     }
     finish_instance<W>(g, a, i, ck, 8, dec_val, dec_round, halt_round, x, &bc);
   }
@@ -154,30 +158,37 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
   counters_flush(&bc, a.counters, 8, a.R);
 }
 
-template <int W>
+template <int W, bool V2>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(otr_kernel<W>, dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  hipLaunchKernelGGL((otr_kernel<W, V2>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_otr(const KArgs& a, int W, int grid, hipStream_t s) {
+template <bool V2>
+static hipError_t launch_v(const KArgs& a, int W, int grid, hipStream_t s) {
   switch (W) {
-    case 1: return launch_w<1>(a, grid, s);
-    case 2: return launch_w<2>(a, grid, s);
-    case 3: return launch_w<3>(a, grid, s);
-    case 4: return launch_w<4>(a, grid, s);
+    case 1: return launch_w<1, V2>(a, grid, s);
+    case 2: return launch_w<2, V2>(a, grid, s);
+    case 3: return launch_w<3, V2>(a, grid, s);
+    case 4: return launch_w<4, V2>(a, grid, s);
   }
   return hipErrorInvalidValue;
 }
 
-const void* otr_kernel_ptr(int W) {
+template <bool V2>
+static const void* ptr_v(int W) {
   switch (W) {
-    case 1: return (const void*)otr_kernel<1>;
-    case 2: return (const void*)otr_kernel<2>;
-    case 3: return (const void*)otr_kernel<3>;
-    case 4: return (const void*)otr_kernel<4>;
+    case 1: return (const void*)otr_kernel<1, V2>;
+    case 2: return (const void*)otr_kernel<2, V2>;
+    case 3: return (const void*)otr_kernel<3, V2>;
+    case 4: return (const void*)otr_kernel<4, V2>;
   }
   return nullptr;
 }
+
+hipError_t launch_otr(const KArgs& a, int W, int grid, hipStream_t s) { return launch_v<false>(a, W, grid, s); }
+hipError_t launch_otr2(const KArgs& a, int W, int grid, hipStream_t s) { return launch_v<true>(a, W, grid, s); }
+const void* otr_kernel_ptr(int W) { return ptr_v<false>(W); }
+const void* otr2_kernel_ptr(int W) { return ptr_v<true>(W); }
 
 }  // namespace psg

@@ -1,0 +1,218 @@
+// psg_slv.hip — ShortLastVoting (3-round LastVoting variant) on gfx950.
+//
+// Reference: example/ShortLastVoting.scala:13-119 (SlvProcess). Phase of three
+// rounds with the coordinator coord(r/4) = (r/4) % n taken literally from the
+// source (r/4 although the phase has 3 rounds, ShortLastVoting.scala:37):
+//   R0  every process sends (x, ts) to the coordinator; with a majority it takes
+//       vote = x of mailbox.maxBy(ts) and commits (shared maxby_ts_x helper);
+//   R1  a committed coordinator broadcasts vote; receivers adopt x = vote, ts = r/4;
+//   R2  processes with ts == r/4 broadcast x; a receiver with a majority decides
+//       mailbox.head._2 (first entry in Scala Map iteration order of ITS mailbox)
+//       and exits; commit is cleared.
+// The R2 head is resolved per receiver: if every R2 sender holds the same x the
+// head's value is that x; otherwise each lane walks the CHAMP trie of its own
+// mailbox (champ_first over a per-block fragment table). The fallback is
+// defensive: an R2 sender at round k = 3φ+2 has ts == k/4, and only the R1 of the
+// same phase (k-1) can have set that ts — (3ψ+1)/4 != (3φ+2)/4 for every ψ < φ
+// because 4 consecutive integers hold a multiple of 4 — so every R2 sender holds
+// that R1's single broadcast vote. champ_first is checked against the oracle's
+// Map order by psg_selftest_map_head.
+// Spec: TrivialSpec; the build checks uniform agreement (k = 1 over every
+// decider, HO-model consensus) and validity.
+#include "psg_device.hpp"
+#include "psg_kernels.hpp"
+
+namespace psg {
+
+enum : uint32_t { S_DECIDED = 1u, S_COMMIT = 2u, S_HALTED = 4u };
+
+template <int W>
+struct SlvLds {
+  int32_t xs[W > 1 ? 64 * W : 1];
+  int32_t votes[W > 1 ? 64 * W : 1];
+  int32_t ds[W > 1 ? 64 * W : 1];
+  uint64_t hos[W > 1 ? 64 * W * W : 1];
+};
+
+// The coordinator's HO mask (uniform).
+template <int W>
+PSG_DEV Mask<W> slv_ho_of(Grp<W>& g, SlvLds<W>& L, const Mask<W>& ho, int c) {
+  Mask<W> m;
+  if constexpr (W == 1) {
+    m.w[0] = readlane64(ho.w[0], c);
+  } else {
+#pragma unroll
+    for (int w = 0; w < W; ++w) L.hos[g.pid * W + w] = ho.w[w];
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < W; ++w) m.w[w] = rfl64(L.hos[c * W + w]);
+    __syncthreads();
+  }
+  return m;
+}
+
+template <int W>
+__global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
+  __shared__ BlockCounters bc;
+  __shared__ uint64_t xb[2 * W];
+  __shared__ int64_t red[2 * W];
+  __shared__ SlvLds<W> L;
+  __shared__ ChampTable<W> CT;
+  __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
+  counters_init(&bc);
+  CT.build(a.n);
+  __syncthreads();
+  Grp<W> g;
+  grp_setup(g, a, xb, red);
+  constexpr int G = Geometry<W>::kGroups;
+  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int n = a.n;
+  const int need2 = a.variant == 1 ? 0 : n / 2;  // R2 quorum (ShortLastVoting.scala:85; variant 1: mutation)
+  const Mask<W> full = mfull<W>(n);
+  const uint32_t myh = scala_improve((uint32_t)g.pid);
+
+  for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
+    const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
+    Sched<W> sc;
+    sc.setup(a, inst, g.pid, g.valid);
+    sc.prep_good(0, g.lane, a.R);
+    int32_t x0 = 0;
+    if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_SLV);
+    X0Set<W> X0;
+    X0.build(g, x0tab[grp], x0);
+    // SlvProcess state after init(io) (ShortLastVoting.scala:15-31)
+    int32_t x = x0, ts = -1, vote = 0, decision = -1;
+    uint32_t fl = g.valid ? 0u : S_HALTED;
+    int32_t dec_val = 0, dec_round = -1, halt_round = -1;
+    Checks ck;
+    ck.reset();
+    auto check = [&](int c) {
+      if constexpr (W > 1) {
+        L.ds[g.pid] = decision;
+        __syncthreads();
+      }
+      kagree_check<W>(g, ck, c, 1, full, (fl & S_DECIDED) != 0u, decision, X0, false, L.ds);
+    };
+    check(0);
+
+    for (int k = 0; k < a.R; ++k) {
+      const Mask<W> act = g.ballot((fl & S_HALTED) == 0u);
+      if (many(act)) {
+        const int32_t r4 = k >> 2;
+        const int c = r4 % n;
+        const bool cAlive = mtest(act, c);
+        const uint32_t live = (fl & S_HALTED) ? 0u : 1u;
+        Mask<W> goodS;
+        const bool good = sc.good_round(k, g.lane, a.R, goodS);
+        Mask<W> CB = mzero<W>(), CN = mzero<W>();
+        if (sc.crash_on) {
+          CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
+          CN = g.ballot(sc.crash_round == k);
+        }
+        const Mask<W> HO = sc.ho(k, g.pid, good, goodS, CB, CN);
+        if constexpr (W > 1) {
+          L.xs[g.pid] = x;
+          L.votes[g.pid] = vote;
+          __syncthreads();
+        }
+        const int m3 = k % 3;
+        if (m3 == 0) {  // R0 (ShortLastVoting.scala:34-47)
+          const Mask<W> Mc = mand(slv_ho_of<W>(g, L, HO, c), act);
+          const int size = mpopc(Mc);
+          if (cAlive && size > n / 2) {
+            const int32_t v = maxby_ts_x<W>(g, L.xs, Mc, size, x, ts, myh, a.tiebreak);
+            if (g.pid == c) {
+              vote = v;
+              fl |= S_COMMIT;
+            }
+          }
+        } else if (m3 == 1) {  // R1 (ShortLastVoting.scala:51-69)
+          const bool sent = cAlive && mtest(g.ballot((fl & S_COMMIT) != 0u), c);
+          if (sent) {
+            const int32_t vc = g.bcast(vote, L.votes, c);
+            const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
+            x = rcv ? vc : x;
+            ts = rcv ? r4 : ts;
+          }
+        } else {  // R2 (ShortLastVoting.scala:72-98)
+          const Mask<W> S = mand(act, g.ballot(ts == r4));
+          const Mask<W> M = mand(HO, S);
+          const bool upd = live && mpopc(M) > need2 && (fl & S_DECIDED) == 0u;
+          if (g.any(upd)) {
+            const int32_t xs0 = g.bcast(x, L.xs, mfirst(S));
+            const bool uniform = !many(mand(S, g.ballot(x != xs0)));
+            int32_t v = xs0;
+            if (!uniform) {
+              const int h = upd ? champ_first<W>(CT, M, a.tiebreak) : g.pid;  // mailbox.head
+              v = g.gather(x, L.xs, h);
+            }
+            if (upd) {
+              dec_val = v;
+              dec_round = k;
+              decision = v;
+              fl |= S_DECIDED;
+            }
+          }
+          if (live) {
+            fl &= ~S_COMMIT;
+            if (fl & S_DECIDED) {
+              fl |= S_HALTED;
+              halt_round = k;
+            }
+          }
+        }
+      }
+      check(k + 1);
+    }
+    finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, x, &bc);
+  }
+  __syncthreads();
+  counters_flush(&bc, a.counters, 2, a.R);
+}
+
+template <int W>
+static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(slv_kernel<W>, dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_slv(const KArgs& a, int W, int grid, hipStream_t s) {
+  switch (W) {
+    case 1: return launch_w<1>(a, grid, s);
+    case 2: return launch_w<2>(a, grid, s);
+    case 3: return launch_w<3>(a, grid, s);
+    case 4: return launch_w<4>(a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+const void* slv_kernel_ptr(int W) {
+  switch (W) {
+    case 1: return (const void*)slv_kernel<1>;
+    case 2: return (const void*)slv_kernel<2>;
+    case 3: return (const void*)slv_kernel<3>;
+    case 4: return (const void*)slv_kernel<4>;
+  }
+  return nullptr;
+}
+
+// Self-test of champ_first (psg_selftest_map_head): one lane per pid set (n <= 64).
+__global__ void __launch_bounds__(256) champ_selftest_kernel(const uint64_t* sets, int count, int tiebreak,
+                                                            int32_t* out) {
+  __shared__ ChampTable<1> CT;
+  CT.build(64);
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) {
+    Mask<1> m;
+    m.w[0] = sets[i];
+    out[i] = champ_first<1>(CT, m, tiebreak);
+  }
+}
+
+hipError_t launch_champ_selftest(const uint64_t* sets, int count, int tiebreak, int32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(champ_selftest_kernel, dim3((count + 255) / 256), dim3(256), 0, s, sets, count, tiebreak, out);
+  return hipGetLastError();
+}
+
+}  // namespace psg

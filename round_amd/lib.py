@@ -22,6 +22,7 @@ EXPORTED_SYMBOLS = [
     "psg_config_default", "psg_check_count", "psg_check_name", "psg_alg_from_class",
     "psg_create", "psg_load_inputs", "psg_run_batch", "psg_copy_decisions",
     "psg_fetch_instances", "psg_last_error", "psg_destroy", "psg_create_error",
+    "psg_selftest_map_head",
 ]
 
 
@@ -59,6 +60,8 @@ def load():
     L.psg_destroy.argtypes = [C.c_void_p]
     L.psg_destroy.restype = None
     L.psg_create_error.restype = C.c_char_p
+    L.psg_selftest_map_head.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
+                                        C.POINTER(C.c_int32)]
     _lib = L
     return L
 
@@ -140,3 +143,16 @@ def loaded_path():
 
 if __name__ == "__main__":  # pragma: no cover
     print(loaded_path(), file=sys.stderr)
+
+
+def selftest_map_head(sets, tiebreak=abi.PSG_TIE_CHAMP, device=0):
+    """First pid of each 64-bit pid set in Scala Map order, computed on the GPU
+    (test hook for the per-receiver mailbox.head helper)."""
+    L = load()
+    k = len(sets)
+    arr = (C.c_uint64 * max(1, k))(*[s & ((1 << 64) - 1) for s in sets])
+    out = (C.c_int32 * max(1, k))()
+    rc = L.psg_selftest_map_head(device, arr, k, tiebreak, out)
+    if rc != 0:
+        raise PsgError(rc, "psg_selftest_map_head failed")
+    return list(out)[:k]

@@ -57,8 +57,9 @@ class Algorithm:
     alg_id = 0
     phase_length = 1  # rounds.length (psync/Process.scala:28)
 
-    def __init__(self, param=0, variant=0):
+    def __init__(self, param=0, variant=0, param2=0):
         self.param = int(param)
+        self.param2 = int(param2)
         self.variant = int(variant)
 
     def default_schedule(self, n):
@@ -153,7 +154,52 @@ class BenOr(Algorithm):
         return 2
 
 
-ALGORITHMS = {c.class_name: c for c in (OTR, LastVoting, FloodMin, KSetAgreement, BenOr)}
+class OTR2(Algorithm):
+    """example.OTR2(rt, timeout, afterDecision = 2) — example/Otr2.scala:69 (decision: Option[Int])."""
+    class_name = "example.OTR2"
+    alg_id = abi.PSG_ALG_OTR2
+
+    def __init__(self, afterDecision=2, variant=0):
+        super().__init__(afterDecision, variant)
+
+
+class ShortLastVoting(Algorithm):
+    """example.ShortLastVoting(rt, timeout) — example/ShortLastVoting.scala:108 (3-round phase)."""
+    class_name = "example.ShortLastVoting"
+    alg_id = abi.PSG_ALG_SLV
+    phase_length = 3
+
+    def default_schedule(self, n):
+        return HOSchedule(drop_log2=4, good_round=0.0, crash_fmax=(n - 1) // 2)
+
+    def default_rounds(self, n):
+        return 30
+
+    def default_value_range(self, n):
+        return 2 ** 15 - 1
+
+
+class KSetEarlyStopping(Algorithm):
+    """example.KSetEarlyStopping(rt, t, k, timeout) — example/KSetEarlyStopping.scala:47
+    (runner defaults t = 2, k = 2, KSetEarlyStopping.scala:63-67)."""
+    class_name = "example.KSetEarlyStopping"
+    alg_id = abi.PSG_ALG_KSET_ES
+
+    def __init__(self, t=2, k=2, variant=0):
+        super().__init__(t, variant, param2=k)
+
+    def default_schedule(self, n):
+        return HOSchedule(drop_log2=0, good_round=0.0, crash_fmax=self.param)  # at most t crashes
+
+    def default_rounds(self, n):
+        return self.param // self.param2 + 2  # everyone decides once r > t/k
+
+    def default_value_range(self, n):
+        return 1_000_000
+
+
+ALGORITHMS = {c.class_name: c for c in (OTR, LastVoting, FloodMin, KSetAgreement, BenOr,
+                                          OTR2, ShortLastVoting, KSetEarlyStopping)}
 
 
 def make_config(alg: Algorithm, n: int, rounds: Optional[int] = None, seed: int = 1,
@@ -173,6 +219,7 @@ def make_config(alg: Algorithm, n: int, rounds: Optional[int] = None, seed: int 
     c.seed = seed & ((1 << 64) - 1)
     c.value_range = alg.default_value_range(n) if value_range is None else value_range
     c.param = alg.param
+    c.param2 = alg.param2
     c.tiebreak = tiebreak
     c.device = device
     c.variant = alg.variant

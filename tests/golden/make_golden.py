@@ -37,6 +37,12 @@ FIXTURES = {
     "c4_kset_n256_k2_f4": (psync.KSetAgreement(2), 256, 8, dict(seed=4, schedule=H(drop_log2=0, good_round=0.0,
                                                                                       crash_fmax=4))),
     "c5_benor_n128": (psync.BenOr(), 128, 100, dict(seed=5)),
+    # second-wave algorithms
+    "w2_otr2_n64_V4": (psync.OTR2(), 64, 200, dict(value_range=4, seed=6)),
+    "w2_slv_n64": (psync.ShortLastVoting(), 64, 200, dict(seed=7)),
+    "w2_slv_n16_loss": (psync.ShortLastVoting(), 16, 400, dict(value_range=5, seed=7, schedule=H(
+        drop_log2=1, good_round=0.0, crash_fmax=7))),
+    "w2_kset_es_n64_t8_k2": (psync.KSetEarlyStopping(8, 2), 64, 200, dict(seed=8)),
 }
 
 BEGIN = 12345

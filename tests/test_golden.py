@@ -28,6 +28,7 @@ def to_cfg(d):
             setattr(c, k, v)
     for k, v in d["sched"].items():
         setattr(c.sched, k, v)
+    c.abi_version = abi.PSG_ABI_VERSION  # fields added by later ABI versions default to 0
     return c
 
 

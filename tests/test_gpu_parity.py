@@ -47,6 +47,25 @@ CASES = [
     ("benor-n4", psync.BenOr(), 4, 3000, dict(seed=26)),
     ("benor-n64-mutant", psync.BenOr(variant=1), 64, 500, dict(seed=27)),
     ("benor-n200-W4", psync.BenOr(), 200, 60, dict(seed=28, rounds=20)),
+    # second wave
+    ("otr2-n64-V4", psync.OTR2(), 64, 2000, dict(value_range=4, seed=40)),
+    ("otr2-mutant-n8", psync.OTR2(variant=1), 8, 3000, dict(schedule=H(drop_log2=1, good_round=0.0), seed=41)),
+    ("otr2-n100-W2", psync.OTR2(), 100, 300, dict(value_range=8, seed=42)),
+    ("slv-n64", psync.ShortLastVoting(), 64, 2000, dict(seed=43)),
+    ("slv-n16-loss", psync.ShortLastVoting(), 16, 3000, dict(value_range=5, seed=44, schedule=H(
+        drop_log2=1, good_round=0.0, crash_fmax=7))),
+    ("slv-mutant-n16", psync.ShortLastVoting(variant=1), 16, 3000, dict(value_range=5, seed=45, schedule=H(
+        drop_log2=1, good_round=0.0, crash_fmax=7))),
+    ("slv-n16-minpid", psync.ShortLastVoting(), 16, 2000, dict(value_range=5, seed=46, tiebreak=abi.PSG_TIE_MIN_PID,
+                                                               schedule=H(drop_log2=1, good_round=0.0))),
+    ("slv-n130-W3", psync.ShortLastVoting(), 130, 100, dict(seed=47)),
+    ("slv-n256-W4-loss", psync.ShortLastVoting(), 256, 40, dict(value_range=3, seed=48,
+                                                                schedule=H(drop_log2=1, good_round=0.0))),
+    ("kses-n64-t8k2", psync.KSetEarlyStopping(8, 2), 64, 1000, dict(seed=49)),
+    ("kses-n256-t16k3", psync.KSetEarlyStopping(16, 3), 256, 100, dict(seed=50)),
+    ("kses-mutant-n16", psync.KSetEarlyStopping(4, 2, variant=1), 16, 3000, dict(seed=51)),
+    ("kses-pureho", psync.KSetEarlyStopping(4, 2), 16, 2000, dict(seed=52, schedule=H(
+        drop_log2=2, good_round=0.0, crash_fmax=4, self_bit=False))),
 ]
 
 
@@ -147,3 +166,23 @@ def test_invalid_config_raises():
     from round_amd import lib
     with pytest.raises(PsgError):
         lib.Context(cfg)
+
+
+def test_gpu_map_head_matches_oracle(oracle_mod):
+    """champ_first (per-receiver mailbox.head, psg_slv.hip) vs the oracle's Scala Map order."""
+    import random
+    from round_amd import lib
+    rng = random.Random(5)
+    sets = [0, 1, 0b11111, (1 << 64) - 1, (1 << 63) | 1]
+    for _ in range(3000):
+        m = 0
+        for q in range(64):
+            if rng.random() < rng.choice([0.05, 0.2, 0.5, 0.9]):
+                m |= 1 << q
+        sets.append(m)
+    for tb in (abi.PSG_TIE_CHAMP, abi.PSG_TIE_MIN_PID):
+        got = lib.selftest_map_head(sets, tb)
+        for m, h in zip(sets, got):
+            pids = [q for q in range(64) if (m >> q) & 1]
+            want = oracle_mod.scala_map_order(pids, tb)[0] if pids else -1
+            assert h == want, (hex(m), tb, h, want)

@@ -5,7 +5,9 @@ oracle is pinned by:
   * executions hand-traced line by line from the Scala sources
     (example/Otr.scala:59-81, example/LastVoting.scala:239-336,
     example/FloodMin.scala:21-31, example/KSetAgreement.scala:113-133,
-    example/BenOr.scala:210-262) on explicit HO schedules;
+    example/BenOr.scala:210-262, example/Otr2.scala:38-61,
+    example/ShortLastVoting.scala:34-98, example/KSetEarlyStopping.scala:29-41)
+    on explicit HO schedules;
   * the reference's own mmor specification (src/test/scala/psync/logic/OtrExample.scala:67-75);
   * published known-answer values of Philox4x32-10 (Random123 kat_vectors) and
     java.util.Random (JDK LCG);
@@ -184,6 +186,75 @@ def test_benor_unanimous_decides(oracle_mod):
     s, rec, tr = oracle_mod.run_explicit(cfg, [1, 1, 1, 1], [[FULL4] * 4] * 4)
     assert [(r.decision, r.decision_round, r.halt_round) for r in rec] == [(1, 2, 2)] * 4
     assert list(s.first_fail)[:5] == [NEVER] * 5
+
+
+# --------------------------------------------------------------------------- second wave
+def test_otr2_option_decision(oracle_mod):
+    """OTR2, init [1,1,1,2], all HO full: round 0 mmor = 1 with 3 > 2*4/3 copies ->
+    decision = Some(1) everywhere; after 2 -> 1 -> 0, exit in round 1. At c = 0
+    Invariant0 holds (|{x == 1}| = 3 > 2, no decision), Invariant1 does not (3 != n)."""
+    cfg = cfg_for(psync.OTR2(), 4, 3)
+    s, rec, tr = oracle_mod.run_explicit(cfg, [1, 1, 1, 2], [[FULL4] * 4] * 3)
+    assert [(r.decision, r.decision_round, r.halt_round, r.final_x) for r in rec] == [(1, 0, 1, 1)] * 4
+    assert list(s.first_fail)[:8] == [NEVER, NEVER, 0, NEVER, NEVER, NEVER, NEVER, NEVER]
+    assert s.term_round == 1
+
+
+def test_otr2_invariant0_not_initially_true(oracle_mod):
+    """OTR2's Invariant0 has no "nobody decided" disjunct: with four distinct values
+    it is false at c = 0 while Safety (Invariant2: decisions agree) holds."""
+    cfg = cfg_for(psync.OTR2(), 4, 2)
+    s, rec, tr = oracle_mod.run_explicit(cfg, [1, 2, 3, 4], [[FULL4] * 4] * 2)
+    assert s.first_fail[0] == NEVER and s.first_fail[1] == 0 and s.first_fail[3] == NEVER
+
+
+def test_kset_early_stopping_two_speeds(oracle_mod):
+    """t = 2, k = 2 (t/k = 1), init [5,3,9,7]. Round 0: p0 hears {0,3} -> est 5,
+    canDecide = 4 - 2 < 2 = false; the others hear everyone -> est 3, canDecide
+    (4 - 4 < 2). Round 1: p1..p3 decide 3 and exit; p0 takes est = 3 and canDecide
+    from their flags. Round 2 (r = 2 > t/k): p0 decides 3."""
+    cfg = cfg_for(psync.KSetEarlyStopping(2, 2), 4, 3, value_range=100)
+    r0 = [0b1001, FULL4, FULL4, FULL4]
+    s, rec, tr = oracle_mod.run_explicit(cfg, [5, 3, 9, 7], [r0, [FULL4] * 4, [FULL4] * 4])
+    assert tr[1][0] == [5, 3, 3, 3]
+    assert [(r.decision, r.decision_round, r.halt_round, r.final_x) for r in rec] == \
+        [(3, 2, 2, 3)] + [(3, 1, 1, 3)] * 3
+    assert s.term_round == 3
+
+
+def test_short_last_voting_one_phase(oracle_mod):
+    """n = 3, all HO full: R0 coord 0 hears 3 > 1 -> vote = x of maxBy ts (all -1:
+    first inserted, pid 0) = 4; R1 everyone adopts x = 4, ts = 0; R2 everyone
+    sends (ts == 2/4 = 0), hears 3 > 1 and decides mailbox.head = 4, then exits."""
+    cfg = cfg_for(psync.ShortLastVoting(), 3, 3, value_range=100)
+    s, rec, tr = oracle_mod.run_explicit(cfg, [4, 7, 2], [[0b111] * 3] * 3)
+    assert tr[2][0] == [4, 4, 4]
+    assert [(r.decision, r.decision_round, r.halt_round, r.final_x) for r in rec] == [(4, 2, 2, 4)] * 3
+
+
+def test_short_last_voting_missed_vote(oracle_mod):
+    """p2 misses the coordinator's R1 broadcast: it keeps (x = 2, ts = -1), does not
+    send in R2, but still decides the head of {0, 1} (value 4)."""
+    cfg = cfg_for(psync.ShortLastVoting(), 3, 3, value_range=100)
+    full = [0b111] * 3
+    s, rec, tr = oracle_mod.run_explicit(cfg, [4, 7, 2], [full, [0b111, 0b111, 0b110], full])
+    assert tr[2][0] == [4, 4, 2]
+    assert [(r.decision, r.decision_round, r.final_x) for r in rec] == [(4, 2, 4), (4, 2, 4), (4, 2, 2)]
+
+
+def test_short_last_voting_maxby_champ_order(oracle_mod):
+    """n = 6: coordinator 0 hears {1..5} in R0 (5 > 4 entries: a CHAMP HashMap), so
+    maxBy over equal ts = -1 returns the first entry in CHAMP order (pid 5), not
+    the smallest pid; everyone then adopts and decides that value."""
+    n = 6
+    cfg = cfg_for(psync.ShortLastVoting(), n, 3, value_range=100)
+    init = [11, 12, 13, 14, 15, 16]
+    full = (1 << n) - 1
+    r0 = [full & ~1] + [full] * (n - 1)
+    first = oracle_mod.scala_map_order(list(range(1, n)))[0]
+    s, rec, tr = oracle_mod.run_explicit(cfg, init, [r0, [full] * n, [full] * n])
+    assert first == 5
+    assert all(r.decision == init[first] and r.decision_round == 2 for r in rec)
 
 
 # --------------------------------------------------------------------------- third-party algorithms

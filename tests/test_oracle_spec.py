@@ -27,6 +27,9 @@ NEVER = abi.PSG_NEVER
     (psync.BenOr(), 4, {}),
     (psync.BenOr(), 7, dict(schedule=H(drop_log2=1, good_round=0.0, ho_min=3))),
     (psync.BenOr(variant=1), 6, {}),
+    (psync.OTR2(), 4, {}),
+    (psync.OTR2(), 6, dict(value_range=3, schedule=H(drop_log2=1))),
+    (psync.OTR2(variant=1), 8, dict(schedule=H(drop_log2=1, good_round=0.0))),
 ], ids=lambda v: getattr(v, "class_name", None) or None)
 def test_lowered_spec_matches_formula_interpreter(alg, n, kw, oracle_mod):
     cfg = psync.make_config(alg, n, seed=11, **kw)
@@ -44,6 +47,12 @@ def test_lowered_spec_matches_formula_interpreter(alg, n, kw, oracle_mod):
     (psync.FloodMin(8), 32, dict(schedule=H(drop_log2=0, good_round=0.0, crash_fmax=8))),
     (psync.KSetAgreement(2), 32, {}),
     (psync.KSetAgreement(3), 24, dict(schedule=H(drop_log2=0, good_round=0.0, crash_fmax=2))),
+    (psync.OTR2(), 64, dict(value_range=64)),
+    (psync.OTR2(), 16, dict(schedule=H(drop_log2=2, crash_fmax=8))),
+    (psync.ShortLastVoting(), 64, {}),
+    (psync.ShortLastVoting(), 16, dict(value_range=5, schedule=H(drop_log2=1, good_round=0.0, crash_fmax=7))),
+    (psync.KSetEarlyStopping(8, 2), 64, {}),
+    (psync.KSetEarlyStopping(4, 2), 16, {}),
 ])
 def test_zero_false_positives(alg, n, kw, oracle_mod):
     cfg = psync.make_config(alg, n, seed=21, **kw)
@@ -75,6 +84,10 @@ def test_benor_violations_only_after_safety_predicate_breaks(n, oracle_mod):
      [0, 3]),
     (psync.BenOr(variant=1), 8, {}, [0, 2]),
     (psync.KSetAgreement(2, variant=1), 16, dict(schedule=H(drop_log2=0, good_round=0.0, crash_fmax=4)), [0]),
+    (psync.OTR2(variant=1), 8, dict(schedule=H(drop_log2=1, good_round=0.0)), [0, 4]),
+    (psync.ShortLastVoting(variant=1), 16, dict(value_range=5, schedule=H(drop_log2=1, good_round=0.0,
+                                                                          crash_fmax=7)), [0]),
+    (psync.KSetEarlyStopping(4, 2, variant=1), 16, {}, [0]),
 ])
 def test_mutants_are_caught(alg, n, kw, slots, oracle_mod):
     cfg = psync.make_config(alg, n, seed=77, **kw)
