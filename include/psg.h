@@ -56,7 +56,8 @@ enum psg_alg {
   /* second wave */
   PSG_ALG_OTR2 = 6,        /* example.OTR2               example/Otr2.scala:9-104 */
   PSG_ALG_SLV = 7,         /* example.ShortLastVoting    example/ShortLastVoting.scala:13-119 */
-  PSG_ALG_KSET_ES = 8      /* example.KSetEarlyStopping  example/KSetEarlyStopping.scala:9-57 */
+  PSG_ALG_KSET_ES = 8,     /* example.KSetEarlyStopping  example/KSetEarlyStopping.scala:9-57 */
+  PSG_ALG_EPSILON = 9      /* example.EpsilonConsensus   example/Epsilon.scala:16-83 (Double values) */
 };
 
 /* Which element of a Scala immutable.Map is "first" (LastVoting maxBy ties,
@@ -102,7 +103,8 @@ typedef struct psg_config {
   int32_t n;            /* processes per instance, 1..PSG_MAX_N */
   int32_t rounds;       /* R rounds executed per instance, 1..PSG_MAX_ROUNDS */
   uint64_t seed;
-  int32_t value_range;  /* synthetic init values uniform in {1..value_range} (BenOr: {false,true}) */
+  int32_t value_range;  /* synthetic init values uniform in {1..value_range} (BenOr: {false,true};
+                           EpsilonConsensus: Double uniform in [0,1) like Random.nextDouble, unused) */
   int32_t param;        /* OTR/OTR2 afterDecision (Otr.scala:89, default 2); FloodMin f (FloodMin.scala:27);
                            KSet k (KSetAgreement.scala:56); KSetEarlyStopping t; others unused */
   int32_t tiebreak;     /* enum psg_tiebreak */
@@ -112,6 +114,7 @@ typedef struct psg_config {
   psg_schedule sched;
   int32_t param2;       /* KSetEarlyStopping k (KSetEarlyStopping.scala:9; param = t) */
   int32_t reserved;
+  double real_param;    /* EpsilonConsensus epsilon (Epsilon.scala:16; param = f) */
 } psg_config;
 
 /* Aggregate result of one batch. All fields are sums over instances (so a
@@ -140,7 +143,9 @@ typedef struct psg_instance_summary {
   uint16_t n_decided;
 } psg_instance_summary;
 
-/* Per-process record (fetch path). */
+/* Per-process record (fetch path). For EpsilonConsensus (Double state) decision
+ * and final_x hold fold32(bits) = low ^ high word of the IEEE-754 bits; the
+ * values themselves come from the _f64 entry points below. */
 typedef struct psg_process_record {
   int32_t decision;       /* value passed to ConsensusIO.decide (BenOr: 0/1); 0 if none */
   int32_t decision_round; /* round k (0-based) of the first decide callback, -1 if none */
@@ -183,6 +188,16 @@ int psg_copy_decisions(psg_ctx* ctx, int32_t* decision, int32_t* decision_round)
  * summaries (k entries) and per-process records (k * n entries, nullable). */
 int psg_fetch_instances(psg_ctx* ctx, const uint64_t* ids, size_t k,
                         psg_instance_summary* sums, psg_process_record* procs);
+
+/* Real-valued algorithms (PSG_ALG_EPSILON, RealConsensusIO, Epsilon.scala:10-13).
+ * Same contracts as the int32 entry points; other algorithms get PSG_EINVAL.
+ * host_init: [count][n] Double initial values, NULL = seeded (uniform [0,1)). */
+int psg_load_inputs_f64(psg_ctx* ctx, uint64_t inst_begin, uint64_t inst_count, const double* host_init);
+/* decision [count][n] (0.0 if none) and decision_round [count][n] of the last batch. */
+int psg_copy_decisions_f64(psg_ctx* ctx, double* decision, int32_t* decision_round);
+/* psg_fetch_instances plus the Double decision and final x of each process ([k][n] each, nullable). */
+int psg_fetch_instances_f64(psg_ctx* ctx, const uint64_t* ids, size_t k, psg_instance_summary* sums,
+                            psg_process_record* procs, double* decision, double* final_x);
 
 const char* psg_last_error(const psg_ctx* ctx);
 void psg_destroy(psg_ctx* ctx);

@@ -43,6 +43,15 @@ def lib():
                                           C.POINTER(abi.InstanceSummary), C.POINTER(abi.ProcessRecord),
                                           C.POINTER(C.c_int64), C.c_int32]
         L.oracle_run_explicit.restype = C.c_int
+        L.oracle_run_real.argtypes = [C.POINTER(abi.Config), C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_double), C.POINTER(abi.Summary),
+                                      C.POINTER(abi.InstanceSummary), C.POINTER(abi.ProcessRecord),
+                                      C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int32]
+        L.oracle_run_real.restype = C.c_int
+        L.oracle_run_explicit_real.argtypes = [C.POINTER(abi.Config), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                               C.POINTER(abi.InstanceSummary), C.POINTER(abi.ProcessRecord),
+                                               C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.oracle_run_explicit_real.restype = C.c_int
         L.oracle_last_error.restype = C.c_char_p
         L.oracle_philox.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.oracle_java_first_boolean.argtypes = [C.c_int64]
@@ -89,6 +98,52 @@ def run(cfg, inst_begin=0, count=1, ids=None, init=None, per_instance=False, rec
                       threads, spec_mode)
     _check(rc)
     return summ, (list(pi) if pi is not None else None), (list(rec) if rec is not None else None)
+
+
+def run_real(cfg, inst_begin=0, count=1, ids=None, init=None, per_instance=False, records=False, threads=1):
+    """Real-valued algorithm (EpsilonConsensus) on the CPU oracle.
+
+    Returns (Summary, [InstanceSummary], [ProcessRecord], decisions, final_x) where the
+    last two are flat [count*n] Double lists (None unless records=True)."""
+    L = lib()
+    if ids is not None:
+        count = len(ids)
+        ids_arr = (C.c_uint64 * count)(*ids)
+    else:
+        ids_arr = None
+    init_arr = None
+    if init is not None:
+        flat = [float(v) for row in init for v in row]
+        init_arr = (C.c_double * len(flat))(*flat)
+    summ = abi.Summary()
+    pi = (abi.InstanceSummary * count)() if per_instance else None
+    cells = count * cfg.n
+    rec = (abi.ProcessRecord * cells)() if records else None
+    dec = (C.c_double * cells)() if records else None
+    fx = (C.c_double * cells)() if records else None
+    rc = L.oracle_run_real(C.byref(cfg), inst_begin, count, ids_arr, init_arr, C.byref(summ), pi, rec, dec, fx,
+                           threads)
+    _check(rc)
+    return (summ, (list(pi) if pi is not None else None), (list(rec) if rec is not None else None),
+            (list(dec) if dec is not None else None), (list(fx) if fx is not None else None))
+
+
+def run_explicit_real(cfg, init, ho):
+    """One real-valued instance with an explicit HO schedule ho[k][p] (n <= 64).
+    Returns (InstanceSummary, [ProcessRecord], decisions, final_x)."""
+    L = lib()
+    n = cfg.n
+    if len(ho) != cfg.rounds or any(len(row) != n for row in ho):
+        raise ValueError("ho must be [rounds][n]")
+    flat = [m & ((1 << 64) - 1) for row in ho for m in row]
+    ho_arr = (C.c_uint64 * len(flat))(*flat)
+    init_arr = (C.c_double * n)(*[float(v) for v in init])
+    s = abi.InstanceSummary()
+    rec = (abi.ProcessRecord * n)()
+    dec = (C.c_double * n)()
+    fx = (C.c_double * n)()
+    _check(L.oracle_run_explicit_real(C.byref(cfg), init_arr, ho_arr, C.byref(s), rec, dec, fx))
+    return s, list(rec), list(dec), list(fx)
 
 
 def run_explicit(cfg, init, ho, spec_mode=SPEC_BOTH):

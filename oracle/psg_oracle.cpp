@@ -13,7 +13,7 @@
  *   - algorithms: example/Otr.scala:13-86, example/LastVoting.scala:80-212,
  *     example/FloodMin.scala:8-36, example/KSetAgreement.scala:21-68, example/BenOr.scala:11-84,
  *     example/Otr2.scala:9-66, example/ShortLastVoting.scala:13-105,
- *     example/KSetEarlyStopping.scala:9-44;
+ *     example/KSetEarlyStopping.scala:9-44, example/Epsilon.scala:16-70 (Double state);
  *   - Spec: psync/Specs.scala:8-27 and the per-algorithm specs (Otr.scala:95-120,
  *     LastVoting.scala:19-70, BenOr.scala:91-115, Otr2.scala:71-96), evaluated two independent ways:
  *     (a) a Formula-tree interpreter mirroring psync/formula/Formula.scala
@@ -41,10 +41,12 @@
 #include <atomic>
 #include <bitset>
 #include <climits>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <limits>
 #include <map>
 #include <memory>
 #include <set>
@@ -231,6 +233,13 @@ struct Schedule {
     uint64_t w = rword(cfg.seed, inst, ROUND_INIT, (uint32_t)p, 0);
     if (cfg.alg == PSG_ALG_BENOR) return (int32_t)((uint32_t)w & 1u);
     return 1 + (int32_t)mulhi32((uint32_t)w, (uint32_t)cfg.value_range);
+  }
+
+  /* RealConsensusIO.initialValue: uniform in [0, 1) with 53 random bits (the
+   * shape of Random.nextDouble, Epsilon.scala:94) */
+  double init_real(int p) const {
+    uint64_t w = rword(cfg.seed, inst, ROUND_INIT, (uint32_t)p, 0);
+    return (double)(w >> 11) * 0x1.0p-53;
   }
 
   bool coin(int k, int p) const {
@@ -532,6 +541,7 @@ static int n_checks_of(int alg) {
     case PSG_ALG_OTR2: return 8;
     case PSG_ALG_SLV: return 2;
     case PSG_ALG_KSET_ES: return 2;
+    case PSG_ALG_EPSILON: return 3;
   }
   return 0;
 }
@@ -568,11 +578,22 @@ static void eval_spec_interp(const SpecDef& sd, const SpecState& st, int L, bool
 /* ------------------------------------------------------------------ */
 /* Algorithms (literal restatements)                                   */
 /* ------------------------------------------------------------------ */
-struct Callback { /* ConsensusIO.decide */
+/* fold32 of the IEEE-754 bits: how a Double enters the int32 record fields and the digest */
+static int32_t fold32(double d) {
+  uint64_t b;
+  std::memcpy(&b, &d, 8);
+  return (int32_t)(uint32_t)(b ^ (b >> 32));
+}
+
+struct Callback { /* ConsensusIO.decide / RealConsensusIO.decide */
   int32_t value = 0;
   int32_t round = -1;
+  double fvalue = 0.0;
   void decide(int32_t v, int k) {
     if (round < 0) { value = v; round = k; }
+  }
+  void decide_real(double v, int k) {
+    if (round < 0) { fvalue = v; value = fold32(v); round = k; }
   }
 };
 
@@ -981,6 +1002,114 @@ struct KSetES {
   int32_t main_x(const P& s) const { return s.est; }
 };
 
+/* ---------------- EpsilonConsensus: example/Epsilon.scala:16-70 ---------------- */
+/* Java narrowing of double to int (math.ceil(r1).toInt). */
+static int32_t d2i(double d) {
+  if (std::isnan(d)) return 0;
+  if (d >= 2147483647.0) return INT32_MAX;
+  if (d <= -2147483648.0) return INT32_MIN;
+  return (int32_t)d;
+}
+/* Ordering.Double.TotalOrdering (java.lang.Double.compare): -0.0 < 0.0, NaN last. */
+static int64_t total_key(double d) {
+  int64_t b;
+  if (std::isnan(d)) b = 0x7ff8000000000000LL; /* doubleToLongBits canonical NaN */
+  else std::memcpy(&b, &d, 8);
+  return b ^ ((b >> 63) & 0x7fffffffffffffffLL);
+}
+
+struct Epsilon {
+  struct P {
+    double x = 0.0;
+    int32_t maxR = 0;                /* var maxR = new Time(0) */
+    std::map<int, double> halted;    /* var halted = Map[ProcessID, Double]() */
+    bool decided = false;
+    double decision = 0.0;
+  };
+  struct Payload { double x; bool flag; };
+  int n, f, variant;
+  double eps;
+  static const int L = 1;
+  void init(P& s, double v) { s.x = v; } /* Epsilon.scala:23-26 */
+  bool sends_to(const P&, int, int, int) const { return true; }
+  /* if (r <= maxR) broadcast(x -> false) else broadcast(x -> true), Epsilon.scala:44-50 */
+  Payload payload(const P& s, int, int k, int) const { return {s.x, !(k <= s.maxR)}; }
+  static std::vector<double> sorted(std::vector<double> v) {
+    std::stable_sort(v.begin(), v.end(), [](double a, double b) { return total_key(a) < total_key(b); });
+    return v;
+  }
+  /* Epsilon.scala:52-67 */
+  bool update(P& s, int, int k, const std::vector<Msg<Payload>>& mb, Callback& cb, const Schedule&, int) {
+    std::vector<double> V;
+    for (auto& m : mb) V.push_back(m.payload.x);          /* mailbox.toSeq.map(_._2._1) */
+    for (auto& kv : s.halted) V.push_back(kv.second);     /* ++ halted.values */
+    for (auto& m : mb) if (m.payload.flag) s.halted[m.src] = m.payload.x;
+    if (k == 0) {
+      /* diff(V) of an empty V and reduce(2f, V).head with |V| <= 4f throw in Scala;
+       * here they leave maxR / x unchanged (needs a pure-HO schedule or tiny mailboxes) */
+      if (V.empty()) return false;
+      std::vector<double> sv = sorted(V);
+      const double diff = sv.back() - sv.front();       /* s.max - s.min */
+      const int c = (n - 3 * f - 1) / (2 * f) + 1;       /* c(n-3f, 2f) = (m-1)/k + 1 */
+      const double r1 = std::log(diff / eps) / std::log((double)c);
+      s.maxR = d2i(std::ceil(r1));
+      if (variant == 1) s.maxR = 0; /* mutation: no approximation rounds, decide in round 1 */
+      if ((int)sv.size() > 4 * f) s.x = sv[2 * f];       /* reduce(2f, V).head */
+    } else if (k <= s.maxR) {
+      /* _new(2f, f, V): red = sorted.drop(f).dropRight(f); sel = red.grouped(2f).map(_.head);
+       * sel.sum / sel.size (left fold from 0.0; 0.0 / 0 = NaN for an empty sel) */
+      std::vector<double> sv = sorted(V);
+      const int m = (int)sv.size();
+      double sum = 0.0;
+      int cnt = 0;
+      for (int j = f; j < m - f; j += 2 * f) { sum += sv[j]; ++cnt; }
+      s.x = sum / (double)cnt;
+    } else {
+      cb.decide_real(s.x, k);
+      s.decided = true;
+      s.decision = s.x;
+      return true;
+    }
+    return false;
+  }
+  void fields(const P& s, int64_t* fv) const {
+    fv[F_X] = fold32(s.x); fv[F_DECIDED] = s.decided; fv[F_DECISION] = fold32(s.decision);
+  }
+  int32_t main_x(const P& s) const { return fold32(s.x); }
+  /* Build-defined checks (TrivialSpec, Epsilon.scala:74): 0 EpsAgreement — decisions
+   * are not NaN and max - min <= epsilon; 1 EpsValidity — every decision lies within
+   * [min, max] of the (non-NaN) initial values; 2 SafetyPredicate — every process
+   * that took a step had |V| = |mailbox| + |halted| >= n - f values (the commented
+   * assert mailbox.size >= n - f, Epsilon.scala:57, with the remembered values of
+   * halted senders standing in for their messages after they exit). */
+  void checks(const std::vector<P>& st, const std::vector<double>& x0, const std::vector<int>& hosize,
+              std::vector<bool>& ck, bool& term) const {
+    bool anyD = false, nanD = false, anyI = false;
+    double mx = 0, mn = 0, lo = 0, hi = 0;
+    for (double v : x0)
+      if (!std::isnan(v)) {
+        if (!anyI) { lo = hi = v; anyI = true; }
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+      }
+    bool valid = true;
+    term = true;
+    for (size_t p = 0; p < st.size(); ++p) {
+      if (!st[p].decided) { term = false; continue; }
+      const double d = st[p].decision;
+      if (std::isnan(d)) { nanD = true; valid = false; continue; }
+      if (!anyD) { mx = mn = d; anyD = true; }
+      mx = d > mx ? d : mx;
+      mn = d < mn ? d : mn;
+      if (!(anyI && lo <= d && d <= hi)) valid = false;
+    }
+    const bool agree = !nanD && (!anyD || mx - mn <= eps);
+    bool pred = true;
+    for (int h : hosize) if (h < n - f) pred = false;
+    ck = {agree, valid, pred};
+  }
+};
+
 /* ------------------------------------------------------------------ */
 /* Hand-lowered Spec evaluator (what the GPU kernel implements)         */
 /* ------------------------------------------------------------------ */
@@ -1155,6 +1284,7 @@ enum SpecMode { SPEC_DIRECT = 0, SPEC_INTERP = 1, SPEC_BOTH = 2 };
 struct InstOut {
   psg_instance_summary sum;
   std::vector<psg_process_record> rec;
+  std::vector<double> fdec, fx; /* real-valued algorithms: Double decision / final x per process */
   std::vector<int64_t> trace; /* optional: per check point, per process F_X / decided */
   bool mismatch = false;
   std::string msg;
@@ -1166,7 +1296,8 @@ struct ExplicitHO { /* test hook: explicit HO masks [R][n] (n <= 64), explicit c
 
 template <class Alg>
 static void run_engine(Alg& alg, const psg_config& cfg, uint64_t inst, const int32_t* init_in, int spec_mode,
-                       const ExplicitHO* eho, InstOut& out, bool want_trace) {
+                       const ExplicitHO* eho, InstOut& out, bool want_trace, const double* init_real = nullptr) {
+  constexpr bool kReal = std::is_same<Alg, Epsilon>::value;
   const int n = cfg.n, R = cfg.rounds;
   Schedule sch(cfg, inst);
   std::vector<typename Alg::P> st(n);
@@ -1174,9 +1305,15 @@ static void run_engine(Alg& alg, const psg_config& cfg, uint64_t inst, const int
   std::vector<bool> halted(n, false);
   std::vector<int32_t> halt_round(n, -1);
   std::vector<int32_t> x0(n);
+  std::vector<double> x0r(n);
   for (int p = 0; p < n; ++p) {
-    x0[p] = init_in ? init_in[p] : sch.init_value(p);
-    alg.init(st[p], x0[p]);
+    if constexpr (kReal) {
+      x0r[p] = init_real ? init_real[p] : sch.init_real(p);
+      alg.init(st[p], x0r[p]);
+    } else {
+      x0[p] = init_in ? init_in[p] : sch.init_value(p);
+      alg.init(st[p], x0[p]);
+    }
   }
   if constexpr (std::is_same<Alg, KSet>::value) /* t = Map(id -> io.initialValue) */
     for (int p = 0; p < n; ++p) st[p].t = {{p, x0[p]}};
@@ -1218,7 +1355,8 @@ static void run_engine(Alg& alg, const psg_config& cfg, uint64_t inst, const int
     std::vector<bool> ck, ck2;
     bool term = false, term2 = false;
     Direct d{n, cfg.alg, cfg.param, cfg.param2, c, fcur, fold, finit, &crashed, has_old};
-    if (spec_mode != SPEC_INTERP) d.eval(ck, term);
+    if constexpr (kReal) alg.checks(st, x0r, hosize, ck, term);
+    else if (spec_mode != SPEC_INTERP) d.eval(ck, term);
     if (spec_mode != SPEC_DIRECT) {
       SpecState ss;
       ss.n = n; ss.r = c;
@@ -1270,6 +1408,8 @@ static void run_engine(Alg& alg, const psg_config& cfg, uint64_t inst, const int
     }
     std::vector<bool> exiting(n, false);
     for (int p = 0; p < n; ++p) hosize[p] = halted[p] ? n : (int)inbox[p].size();
+    if constexpr (kReal) /* Epsilon: |V| = |mailbox| + |halted| (disjoint: a halted sender is silent) */
+      for (int p = 0; p < n; ++p) if (!halted[p]) hosize[p] += (int)st[p].halted.size();
     for (int p = 0; p < n; ++p) {
       if (halted[p]) continue;
       std::vector<Msg<Payload>> mb;
@@ -1290,6 +1430,10 @@ static void run_engine(Alg& alg, const psg_config& cfg, uint64_t inst, const int
     pr.decision_round = cb[p].round;
     pr.halt_round = halt_round[p];
     pr.final_x = alg.main_x(st[p]);
+    if constexpr (kReal) {
+      out.fdec.push_back(cb[p].fvalue);
+      out.fx.push_back(st[p].x);
+    }
     if (cb[p].round >= 0) ++nd;
     dig += proc_digest(p, pr.decision, pr.decision_round, pr.halt_round, pr.final_x);
   }
@@ -1301,15 +1445,21 @@ static int validate(const psg_config* c, std::string& err) {
   if (!c) { err = "null config"; return PSG_EINVAL; }
   if (c->n < 1 || c->n > PSG_MAX_N) { err = "n out of range"; return PSG_EINVAL; }
   if (c->rounds < 1 || c->rounds > PSG_MAX_ROUNDS) { err = "rounds out of range"; return PSG_EINVAL; }
-  if (c->alg < PSG_ALG_OTR || c->alg > PSG_ALG_KSET_ES) { err = "unknown alg"; return PSG_EINVAL; }
+  if (c->alg < PSG_ALG_OTR || c->alg > PSG_ALG_EPSILON) { err = "unknown alg"; return PSG_EINVAL; }
   if (c->alg == PSG_ALG_KSET_ES && (c->param < 0 || c->param2 < 1)) { err = "KSetEarlyStopping needs t >= 0, k >= 1"; return PSG_EINVAL; }
-  if (c->alg != PSG_ALG_BENOR && c->value_range < 1) { err = "value_range < 1"; return PSG_EINVAL; }
+  if (c->alg == PSG_ALG_EPSILON && (c->param < 1 || !(c->real_param > 0.0))) { err = "EpsilonConsensus needs f >= 1, epsilon > 0"; return PSG_EINVAL; }
+  if (c->alg != PSG_ALG_BENOR && c->alg != PSG_ALG_EPSILON && c->value_range < 1) { err = "value_range < 1"; return PSG_EINVAL; }
   return 0;
 }
 
 static void run_one(const psg_config& cfg, uint64_t inst, const int32_t* init, int spec_mode, const ExplicitHO* eho,
-                    InstOut& out, bool trace) {
+                    InstOut& out, bool trace, const double* init_real = nullptr) {
   switch (cfg.alg) {
+    case PSG_ALG_EPSILON: {
+      Epsilon a{cfg.n, cfg.param, cfg.variant, cfg.real_param};
+      run_engine(a, cfg, inst, init, spec_mode, eho, out, trace, init_real);
+      break;
+    }
     case PSG_ALG_OTR: { Otr a{cfg.n, cfg.param, cfg.variant}; run_engine(a, cfg, inst, init, spec_mode, eho, out, trace); break; }
     case PSG_ALG_LAST_VOTING: { LV a{cfg.n, cfg.variant, cfg.tiebreak}; run_engine(a, cfg, inst, init, spec_mode, eho, out, trace); break; }
     case PSG_ALG_FLOODMIN: { FloodMin a{cfg.n, cfg.param, cfg.variant}; run_engine(a, cfg, inst, init, spec_mode, eho, out, trace); break; }
@@ -1369,9 +1519,28 @@ int32_t oracle_crash_round(const psg_config* cfg, uint64_t inst, int32_t p) {
  * `threads` host threads. init: optional [count][n]; per_inst/recs optional.
  * spec_mode: 0 hand-lowered, 1 Formula interpreter, 2 both (returns -EIO on
  * any disagreement). */
+static int run_impl(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const uint64_t* ids,
+                    const int32_t* init, const double* init_real, psg_summary* out, psg_instance_summary* per_inst,
+                    psg_process_record* recs, double* fdec, double* fx, int32_t threads, int32_t spec_mode);
+
 int oracle_run(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const uint64_t* ids,
                const int32_t* init, psg_summary* out, psg_instance_summary* per_inst,
                psg_process_record* recs, int32_t threads, int32_t spec_mode) {
+  return run_impl(cfg, inst_begin, count, ids, init, nullptr, out, per_inst, recs, nullptr, nullptr, threads,
+                  spec_mode);
+}
+
+/* Real-valued algorithms: Double initial values (nullable = seeded) and the Double
+ * decision / final x of every process ([count][n] each, nullable). */
+int oracle_run_real(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const uint64_t* ids,
+                    const double* init, psg_summary* out, psg_instance_summary* per_inst,
+                    psg_process_record* recs, double* fdec, double* fx, int32_t threads) {
+  return run_impl(cfg, inst_begin, count, ids, nullptr, init, out, per_inst, recs, fdec, fx, threads, 0);
+}
+
+static int run_impl(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const uint64_t* ids,
+                    const int32_t* init, const double* init_real, psg_summary* out, psg_instance_summary* per_inst,
+                    psg_process_record* recs, double* fdec, double* fx, int32_t threads, int32_t spec_mode) {
   std::string err;
   int rc = orc::validate(cfg, err);
   if (rc) { g_oracle_err = err; return rc; }
@@ -1387,7 +1556,8 @@ int oracle_run(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const
     for (uint64_t i = lo; i < hi; ++i) {
       uint64_t inst = ids ? ids[i] : inst_begin + i;
       orc::InstOut o;
-      orc::run_one(*cfg, inst, init ? init + i * (uint64_t)n : nullptr, spec_mode, nullptr, o, false);
+      orc::run_one(*cfg, inst, init ? init + i * (uint64_t)n : nullptr, spec_mode, nullptr, o, false,
+                   init_real ? init_real + i * (uint64_t)n : nullptr);
       if (o.mismatch) { bad = 1; errs[t] = o.msg; }
       s.instances += 1;
       s.process_rounds += (int64_t)n * R;
@@ -1397,6 +1567,8 @@ int oracle_run(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const
       s.term_hist[o.sum.term_round == PSG_NEVER ? R + 1 : o.sum.term_round] += 1;
       if (per_inst) per_inst[i] = o.sum;
       if (recs) std::memcpy(recs + i * (uint64_t)n, o.rec.data(), sizeof(psg_process_record) * n);
+      if (fdec && !o.fdec.empty()) std::memcpy(fdec + i * (uint64_t)n, o.fdec.data(), sizeof(double) * n);
+      if (fx && !o.fx.empty()) std::memcpy(fx + i * (uint64_t)n, o.fx.data(), sizeof(double) * n);
     }
   };
   std::vector<std::thread> th;
@@ -1423,6 +1595,23 @@ int oracle_run(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const
 
 /* Single instance with an explicit HO schedule ho[R][n] (n <= 64) and init
  * values; trace receives (R+1) * 2n int64 (x then decided per check point). */
+/* Explicit HO schedule for a real-valued algorithm: Double init [n]; fdec / fx [n]. */
+int oracle_run_explicit_real(const psg_config* cfg, const double* init, const uint64_t* ho, psg_instance_summary* sum,
+                             psg_process_record* recs, double* fdec, double* fx) {
+  std::string err;
+  int rc = orc::validate(cfg, err);
+  if (rc) { g_oracle_err = err; return rc; }
+  if (cfg->n > 64) { g_oracle_err = "explicit HO needs n <= 64"; return PSG_EINVAL; }
+  orc::ExplicitHO e{ho};
+  orc::InstOut o;
+  orc::run_one(*cfg, 0, nullptr, 0, &e, o, false, init);
+  if (sum) *sum = o.sum;
+  if (recs) std::memcpy(recs, o.rec.data(), sizeof(psg_process_record) * cfg->n);
+  if (fdec && !o.fdec.empty()) std::memcpy(fdec, o.fdec.data(), sizeof(double) * cfg->n);
+  if (fx && !o.fx.empty()) std::memcpy(fx, o.fx.data(), sizeof(double) * cfg->n);
+  return 0;
+}
+
 int oracle_run_explicit(const psg_config* cfg, const int32_t* init, const uint64_t* ho, psg_instance_summary* sum,
                         psg_process_record* recs, int64_t* trace, int32_t spec_mode) {
   std::string err;

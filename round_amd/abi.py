@@ -15,6 +15,7 @@ PSG_ALG_BENOR = 5
 PSG_ALG_OTR2 = 6
 PSG_ALG_SLV = 7
 PSG_ALG_KSET_ES = 8
+PSG_ALG_EPSILON = 9
 
 PSG_TIE_CHAMP = 0
 PSG_TIE_MIN_PID = 1
@@ -42,6 +43,7 @@ CLASS_TO_ALG = {
     "example.OTR2": PSG_ALG_OTR2,
     "example.ShortLastVoting": PSG_ALG_SLV,
     "example.KSetEarlyStopping": PSG_ALG_KSET_ES,
+    "example.EpsilonConsensus": PSG_ALG_EPSILON,
 }
 
 # Check-slot names per algorithm (psg_check_name). Slot 0 of OTR/LV/BenOr is
@@ -58,6 +60,7 @@ CHECK_NAMES = {
                    "Agreement", "Validity", "Integrity", "Irrevocability"],
     PSG_ALG_SLV: ["KAgreement", "KValidity"],
     PSG_ALG_KSET_ES: ["KAgreement", "KValidity"],
+    PSG_ALG_EPSILON: ["EpsAgreement", "EpsValidity", "SafetyPredicate"],
 }
 # Slots whose falsity is a violation (invariant slots are informational: an
 # individual invariant of a sequence legitimately fails before/after its phase;
@@ -72,6 +75,7 @@ VIOLATION_SLOTS = {
     PSG_ALG_OTR2: [0, 4, 5, 6, 7],
     PSG_ALG_SLV: [0, 1],
     PSG_ALG_KSET_ES: [0, 1],
+    PSG_ALG_EPSILON: [0, 1],
 }
 
 
@@ -102,6 +106,7 @@ class Config(C.Structure):
         ("sched", Schedule),
         ("param2", C.c_int32),
         ("reserved", C.c_int32),
+        ("real_param", C.c_double),
     ]
 
 

@@ -50,6 +50,10 @@ struct psg_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint64_t cap = 0;
   int32_t* d_init = nullptr;
+  double* d_init_f64 = nullptr;  // EpsilonConsensus: staged host Double inputs
+  bool init_f64_host = false;    // false: seeded Doubles generated inside the round kernel
+  double* d_dec_f64 = nullptr;
+  double* d_rec_f64 = nullptr;   // fetch path: [k][n][2] (decision, final x)
   bool staged = false;
   uint64_t staged_begin = 0, staged_count = 0;
   int32_t* d_dec = nullptr;
@@ -76,6 +80,7 @@ static int n_checks(int alg) {
     case PSG_ALG_OTR2: return 8;
     case PSG_ALG_SLV: return 2;
     case PSG_ALG_KSET_ES: return 2;
+    case PSG_ALG_EPSILON: return 3;
   }
   return 0;
 }
@@ -86,6 +91,7 @@ static const char* const k_names_lv[] = {"Safety", "Invariant0", "Invariant1", "
                                          "Validity", "Integrity", "Irrevocability"};
 static const char* const k_names_benor[] = {"Safety", "Invariant0", "Agreement", "Irrevocability", "SafetyPredicate"};
 static const char* const k_names_k[] = {"KAgreement", "KValidity"};
+static const char* const k_names_eps[] = {"EpsAgreement", "EpsValidity", "SafetyPredicate"};
 
 static int fail(psg_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -113,6 +119,7 @@ static hipError_t launch_alg(const psg_ctx* c, const KArgs& a, int grid) {
     case PSG_ALG_OTR2: return launch_otr2(a, c->W, grid, c->stream);
     case PSG_ALG_SLV: return launch_slv(a, c->W, grid, c->stream);
     case PSG_ALG_KSET_ES: return launch_kset_es(a, c->W, grid, c->stream);
+    case PSG_ALG_EPSILON: return launch_epsilon(a, c->W, grid, c->stream);
   }
   return hipErrorInvalidValue;
 }
@@ -127,6 +134,7 @@ static const void* kernel_ptr(int alg, int W) {
     case PSG_ALG_OTR2: return otr2_kernel_ptr(W);
     case PSG_ALG_SLV: return slv_kernel_ptr(W);
     case PSG_ALG_KSET_ES: return kset_es_kernel_ptr(W);
+    case PSG_ALG_EPSILON: return epsilon_kernel_ptr(W);
   }
   return nullptr;
 }
@@ -141,6 +149,7 @@ static KArgs make_args(const psg_ctx* c) {
   a.V = f.value_range;
   a.param = f.param;
   a.param2 = f.param2;
+  a.real_param = f.real_param;
   a.variant = f.variant;
   a.tiebreak = f.tiebreak;
   a.drop_log2 = f.sched.drop_log2;
@@ -243,6 +252,14 @@ int psg_config_default(psg_config* cfg, int32_t alg, int32_t n) {
       cfg->sched.good_p32 = 0;
       cfg->sched.crash_fmax = (n - 1) / 2;
       break;
+    case PSG_ALG_EPSILON:  // f = 1, epsilon = 0.1 (Epsilon.scala:83-89)
+      cfg->param = 1;
+      cfg->real_param = 0.1;
+      cfg->rounds = 12;
+      cfg->sched.drop_log2 = 4;
+      cfg->sched.good_p32 = 0;
+      cfg->sched.ho_min = n - 2;  // |HO(p)| >= n - f
+      break;
     case PSG_ALG_KSET_ES:  // t = 2, k = 2 (KSetEarlyStopping.scala:63-67)
       cfg->param = 2;
       cfg->param2 = 2;
@@ -266,6 +283,7 @@ const char* psg_check_name(int32_t alg, int32_t slot) {
     case PSG_ALG_OTR2: return k_names_otr[slot];
     case PSG_ALG_LAST_VOTING: return k_names_lv[slot];
     case PSG_ALG_BENOR: return k_names_benor[slot];
+    case PSG_ALG_EPSILON: return k_names_eps[slot];
     default: return k_names_k[slot];
   }
 }
@@ -276,7 +294,8 @@ int psg_alg_from_class(const char* name) {
       {"example.OTR", PSG_ALG_OTR}, {"example.LastVoting", PSG_ALG_LAST_VOTING},
       {"example.FloodMin", PSG_ALG_FLOODMIN}, {"example.KSetAgreement", PSG_ALG_KSET},
       {"example.BenOr", PSG_ALG_BENOR}, {"example.OTR2", PSG_ALG_OTR2},
-      {"example.ShortLastVoting", PSG_ALG_SLV}, {"example.KSetEarlyStopping", PSG_ALG_KSET_ES}};
+      {"example.ShortLastVoting", PSG_ALG_SLV}, {"example.KSetEarlyStopping", PSG_ALG_KSET_ES},
+      {"example.EpsilonConsensus", PSG_ALG_EPSILON}};
   for (auto& t : tab)
     if (std::strcmp(t.n, name) == 0) return t.id;
   return PSG_EINVAL;
@@ -310,10 +329,17 @@ int psg_selftest_map_head(int32_t device, const uint64_t* sets, int32_t count, i
 static int validate(const psg_config* cfg, std::string& m) {
   if (!cfg) { m = "null config"; return PSG_EINVAL; }
   if (cfg->abi_version != PSG_ABI_VERSION) { m = "ABI version mismatch"; return PSG_EINVAL; }
-  if (cfg->alg < PSG_ALG_OTR || cfg->alg > PSG_ALG_KSET_ES) { m = "unknown algorithm"; return PSG_EINVAL; }
+  if (cfg->alg < PSG_ALG_OTR || cfg->alg > PSG_ALG_EPSILON) { m = "unknown algorithm"; return PSG_EINVAL; }
   if (cfg->n < 1 || cfg->n > PSG_MAX_N) { m = "n out of range 1..256"; return PSG_EINVAL; }
   if (cfg->rounds < 1 || cfg->rounds > PSG_MAX_ROUNDS) { m = "rounds out of range 1..250"; return PSG_EINVAL; }
-  if (cfg->alg != PSG_ALG_BENOR && cfg->value_range < 1) { m = "value_range must be >= 1"; return PSG_EINVAL; }
+  if (cfg->alg != PSG_ALG_BENOR && cfg->alg != PSG_ALG_EPSILON && cfg->value_range < 1) {
+    m = "value_range must be >= 1";
+    return PSG_EINVAL;
+  }
+  if (cfg->alg == PSG_ALG_EPSILON && (cfg->param < 1 || !(cfg->real_param > 0.0))) {
+    m = "EpsilonConsensus needs f >= 1 and epsilon > 0";
+    return PSG_EINVAL;
+  }
   if (cfg->alg == PSG_ALG_KSET && cfg->param < 1) { m = "KSetAgreement needs k >= 1"; return PSG_EINVAL; }
   if (cfg->alg == PSG_ALG_FLOODMIN && cfg->param < 0) { m = "FloodMin needs f >= 0"; return PSG_EINVAL; }
   if ((cfg->alg == PSG_ALG_OTR || cfg->alg == PSG_ALG_OTR2) && cfg->param < 1) {
@@ -356,7 +382,12 @@ int psg_create(psg_ctx** out, const psg_config* cfg) {
   CK(hipEventCreate(&c->ev0));
   CK(hipEventCreate(&c->ev1));
   const uint64_t cells = c->cap * (uint64_t)cfg->n;
-  CK(hipMalloc(&c->d_init, sizeof(int32_t) * cells));
+  if (cfg->alg == PSG_ALG_EPSILON) {
+    CK(hipMalloc(&c->d_init_f64, sizeof(double) * cells));
+    CK(hipMalloc(&c->d_dec_f64, sizeof(double) * cells));
+  } else {
+    CK(hipMalloc(&c->d_init, sizeof(int32_t) * cells));
+  }
   CK(hipMalloc(&c->d_dec, sizeof(int32_t) * cells));
   CK(hipMalloc(&c->d_dround, sizeof(uint8_t) * cells));
   CK(hipMalloc(&c->d_inst, sizeof(psg_instance_summary) * c->cap));
@@ -377,6 +408,10 @@ int psg_create(psg_ctx** out, const psg_config* cfg) {
 int psg_load_inputs(psg_ctx* c, uint64_t inst_begin, uint64_t count, const int32_t* host_init) {
   if (!c) return PSG_EINVAL;
   if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  if (c->cfg.alg == PSG_ALG_EPSILON) {
+    if (host_init) return fail(c, PSG_EINVAL, "EpsilonConsensus takes Double inputs: use psg_load_inputs_f64");
+    return psg_load_inputs_f64(c, inst_begin, count, nullptr);
+  }
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const uint64_t cells = count * (uint64_t)c->cfg.n;
   if (host_init) {
@@ -386,6 +421,23 @@ int psg_load_inputs(psg_ctx* c, uint64_t inst_begin, uint64_t count, const int32
                               c->stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->staged = true;
+  c->staged_begin = inst_begin;
+  c->staged_count = count;
+  return PSG_OK;
+}
+
+int psg_load_inputs_f64(psg_ctx* c, uint64_t inst_begin, uint64_t count, const double* host_init) {
+  if (!c) return PSG_EINVAL;
+  if (c->cfg.alg != PSG_ALG_EPSILON) return fail(c, PSG_EINVAL, "Double inputs are for EpsilonConsensus only");
+  if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (host_init) {
+    const uint64_t cells = count * (uint64_t)c->cfg.n;
+    HIPCHK(c, hipMemcpyAsync(c->d_init_f64, host_init, sizeof(double) * cells, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  c->init_f64_host = host_init != nullptr;
   c->staged = true;
   c->staged_begin = inst_begin;
   c->staged_count = count;
@@ -408,6 +460,11 @@ int psg_run_batch(psg_ctx* c, uint64_t inst_begin, uint64_t count, psg_summary* 
   a.inst_begin = inst_begin;
   a.count = count;
   a.init = c->d_init;
+  if (c->cfg.alg == PSG_ALG_EPSILON) {
+    a.init = nullptr;
+    a.init_f64 = c->init_f64_host ? c->d_init_f64 : nullptr;  // else seeded inside the kernel
+    a.out_dec_f64 = c->d_dec_f64;
+  }
   a.out_decision = c->d_dec;
   a.out_dround = c->d_dround;
   a.out_inst = c->d_inst;
@@ -436,8 +493,31 @@ int psg_copy_decisions(psg_ctx* c, int32_t* decision, int32_t* decision_round) {
   return PSG_OK;
 }
 
+int psg_copy_decisions_f64(psg_ctx* c, double* decision, int32_t* decision_round) {
+  if (!c) return PSG_EINVAL;
+  if (c->cfg.alg != PSG_ALG_EPSILON) return fail(c, PSG_EINVAL, "Double decisions are for EpsilonConsensus only");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const uint64_t cells = c->last_count * (uint64_t)c->cfg.n;
+  if (decision) HIPCHK(c, hipMemcpy(decision, c->d_dec_f64, sizeof(double) * cells, hipMemcpyDeviceToHost));
+  return decision_round ? psg_copy_decisions(c, nullptr, decision_round) : PSG_OK;
+}
+
+static int fetch_impl(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_summary* sums,
+                      psg_process_record* procs, double* fdec, double* fx);
+
 int psg_fetch_instances(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_summary* sums,
                         psg_process_record* procs) {
+  return fetch_impl(c, ids, k, sums, procs, nullptr, nullptr);
+}
+
+int psg_fetch_instances_f64(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_summary* sums,
+                            psg_process_record* procs, double* decision, double* final_x) {
+  if (c && c->cfg.alg != PSG_ALG_EPSILON) return fail(c, PSG_EINVAL, "Double records are for EpsilonConsensus only");
+  return fetch_impl(c, ids, k, sums, procs, decision, final_x);
+}
+
+static int fetch_impl(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_summary* sums,
+                      psg_process_record* procs, double* fdec, double* fx) {
   if (!c || (!ids && k)) return PSG_EINVAL;
   if (k == 0) return PSG_OK;
   if (k > c->cap) return fail(c, PSG_ERANGE, "fetch count exceeds batch_capacity");
@@ -450,6 +530,11 @@ int psg_fetch_instances(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_
     c->fetch_cap = 0;
     HIPCHK(c, hipMalloc(&c->d_ids, sizeof(uint64_t) * k));
     HIPCHK(c, hipMalloc(&c->d_rec, sizeof(psg_process_record) * k * (uint64_t)c->cfg.n));
+    if (c->cfg.alg == PSG_ALG_EPSILON) {
+      if (c->d_rec_f64) (void)hipFree(c->d_rec_f64);
+      c->d_rec_f64 = nullptr;
+      HIPCHK(c, hipMalloc(&c->d_rec_f64, sizeof(double) * 2 * k * (uint64_t)c->cfg.n));
+    }
     c->fetch_cap = k;
   }
   HIPCHK(c, hipMemcpyAsync(c->d_ids, ids, sizeof(uint64_t) * k, hipMemcpyHostToDevice, c->stream));
@@ -460,8 +545,21 @@ int psg_fetch_instances(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_
   a.init = nullptr;  // seeded inputs of each listed id
   a.out_inst = c->d_inst;
   a.out_rec = c->d_rec;
+  a.out_rec_f64 = c->d_rec_f64;
   int rc = run_kernel(c, a, k, nullptr, false);
   if (rc) return rc;
+  if (fdec || fx) {
+    const uint64_t cells = k * (uint64_t)c->cfg.n;
+    double* tmp = new (std::nothrow) double[2 * cells];
+    if (!tmp) return fail(c, PSG_ENOMEM, "host allocation failed");
+    hipError_t e = hipMemcpy(tmp, c->d_rec_f64, sizeof(double) * 2 * cells, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) { delete[] tmp; return hip_fail(c, e, "hipMemcpy(rec_f64)"); }
+    for (uint64_t j = 0; j < cells; ++j) {
+      if (fdec) fdec[j] = tmp[2 * j];
+      if (fx) fx[j] = tmp[2 * j + 1];
+    }
+    delete[] tmp;
+  }
   if (sums) HIPCHK(c, hipMemcpy(sums, c->d_inst, sizeof(psg_instance_summary) * k, hipMemcpyDeviceToHost));
   if (procs)
     HIPCHK(c, hipMemcpy(procs, c->d_rec, sizeof(psg_process_record) * k * (uint64_t)c->cfg.n, hipMemcpyDeviceToHost));
@@ -481,6 +579,9 @@ void psg_destroy(psg_ctx* c) {
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->d_ids) (void)hipFree(c->d_ids);
   if (c->d_rec) (void)hipFree(c->d_rec);
+  if (c->d_init_f64) (void)hipFree(c->d_init_f64);
+  if (c->d_dec_f64) (void)hipFree(c->d_dec_f64);
+  if (c->d_rec_f64) (void)hipFree(c->d_rec_f64);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -29,6 +29,10 @@ struct KArgs {
   psg_process_record* out_rec;       // nullable: [count][n]
   unsigned long long* counters;      // [NCOUNTERS]
   uint64_t seed;
+  const double* init_f64;            // nullable: [count][n] Double initial values (EpsilonConsensus)
+  double* out_dec_f64;               // nullable: [count][n] Double decisions
+  double* out_rec_f64;               // nullable: [count][n][2] (decision, final x) for the fetch path
+  double real_param;                 // EpsilonConsensus epsilon
   int32_t n, R, V, param, param2, variant, tiebreak;
   uint32_t drop_log2, good_p32;
   int32_t good_min, crash_fmax, ho_min;

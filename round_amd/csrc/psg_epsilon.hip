@@ -1,0 +1,229 @@
+// psg_epsilon.hip — EpsilonConsensus (approximate agreement on Doubles) on gfx950.
+//
+// Reference: example/Epsilon.scala:16-70 (EpsilonProcess). One round: broadcast
+// (x, r > maxR); V = mailbox values ++ halted.values; at r = 0
+// maxR = ceil(log(diff(V)/eps) / log(c(n-3f, 2f))) and x = reduce(2f, V).head;
+// while r <= maxR, x = mean of every 2f-th element of V sorted with its f lowest
+// and f highest dropped; afterwards decide(x) and exit.
+//
+// Per round the group sorts all n current values once (rank by a 64-bit
+// Double.compare total-order key, scatter to LDS), and every lane walks the
+// sorted list keeping only the members of its own V: its mailbox plus the
+// halted senders it heard announce (a per-lane pid mask; a halted process's x is
+// frozen, so the value it announced is its current x). Every arithmetic step is
+// the IEEE operation the Scala code performs in the same order (ascending left
+// fold from 0.0, one division), so values match the oracle bit for bit; only
+// log() can differ by an ulp between libm implementations, which moves maxR
+// only when r1 is within an ulp of an integer (parity tolerance in the tests).
+#include "psg_device.hpp"
+#include "psg_kernels.hpp"
+
+namespace psg {
+
+// java.lang.Double.compare order as a signed 64-bit key (-0.0 < 0.0, canonical NaN last)
+PSG_DEV int64_t total_key(double d) {
+  int64_t b = __double_as_longlong(d);
+  if (d != d) b = 0x7ff8000000000000LL;
+  return b ^ ((b >> 63) & 0x7fffffffffffffffLL);
+}
+PSG_DEV double key_value(int64_t k) { return __longlong_as_double(k ^ ((k >> 63) & 0x7fffffffffffffffLL)); }
+
+// Java narrowing double -> int (math.ceil(r1).toInt)
+PSG_DEV int32_t d2i(double d) {
+  if (d != d) return 0;
+  if (d >= 2147483647.0) return INT32_MAX;
+  if (d <= -2147483648.0) return INT32_MIN;
+  return (int32_t)d;
+}
+
+PSG_DEV int32_t fold32d(double d) {
+  const uint64_t b = (uint64_t)__double_as_longlong(d);
+  return (int32_t)(uint32_t)(b ^ (b >> 32));
+}
+
+template <int W>
+struct EpsLds {
+  double sx[Geometry<W>::kGroups][64 * W];
+  int32_t spid[Geometry<W>::kGroups][64 * W];
+  int64_t keys[W > 1 ? 64 * W : 1];
+};
+
+// Slots: 0 EpsAgreement (no NaN decision, max - min <= eps), 1 EpsValidity (every
+// decision within [min, max] of the non-NaN initial values), 2 SafetyPredicate
+// (|V| >= n - f for every process that took a step). Termination: all decided.
+template <int W>
+PSG_DEV void eps_check(Grp<W>& g, Checks& ck, int c, const Mask<W>& full, bool decided, double decision, double eps,
+                       bool anyI, double lo, double hi, bool pred) {
+  const bool nanD = g.any(decided && decision != decision);
+  const bool ok = decided && decision == decision;
+  const bool anyD = g.any(ok);
+  const int64_t kd = total_key(decision);
+  const double mx = key_value(g.max64(kd, ok));
+  const double mn = key_value(g.min64(kd, ok));
+  const bool agree = !nanD && (!anyD || mx - mn <= eps);
+  const bool valid = !g.any(decided && !(anyI && lo <= decision && decision <= hi));
+  ck.record(fbit(agree, 0) | fbit(valid, 1) | fbit(pred, 2), meq(g.ballot(decided), full), c, g.lane);
+}
+
+template <int W>
+__global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a) {
+  __shared__ BlockCounters bc;
+  __shared__ uint64_t xb[2 * W];
+  __shared__ int64_t red[2 * W];
+  __shared__ EpsLds<W> L;
+  counters_init(&bc);
+  __syncthreads();
+  Grp<W> g;
+  grp_setup(g, a, xb, red);
+  constexpr int G = Geometry<W>::kGroups;
+  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int n = a.n;
+  const int f = a.param;
+  const double eps = a.real_param;
+  const double logc = log((double)((n - 3 * f - 1) / (2 * f) + 1));  // log(c(n-3f, 2f))
+  const Mask<W> full = mfull<W>(n);
+  double* sx = L.sx[grp];
+  int32_t* spid = L.spid[grp];
+
+  for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
+    const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
+    Sched<W> sc;
+    sc.setup(a, inst, g.pid, g.valid);
+    sc.prep_good(0, g.lane, a.R);
+    double x0 = 0.0;
+    if (g.valid) {
+      if (a.init_f64) {
+        x0 = a.init_f64[i * (uint64_t)n + g.pid];
+      } else {  // uniform [0,1) with 53 bits (Random.nextDouble shape, Epsilon.scala:94)
+        const uint64_t w = rword(a.seed, inst, ROUND_INIT, (uint32_t)g.pid, 0);
+        x0 = (double)(w >> 11) * 0x1.0p-53;
+      }
+    }
+    const bool inOk = g.valid && x0 == x0;
+    const bool anyI = g.any(inOk);
+    const double lo = key_value(g.min64(total_key(x0), inOk));
+    const double hi = key_value(g.max64(total_key(x0), inOk));
+    // EpsilonProcess state after init(io) (Epsilon.scala:18-26)
+    double x = x0, decision = 0.0;
+    int32_t maxR = 0;
+    Mask<W> H = mzero<W>();  // keys of the `halted` map
+    bool halted = !g.valid, decided = false;
+    int32_t dec_round = -1, halt_round = -1;
+    Checks ck;
+    ck.reset();
+    eps_check<W>(g, ck, 0, full, decided, decision, eps, anyI, lo, hi, true);
+
+    for (int k = 0; k < a.R; ++k) {
+      const Mask<W> act = g.ballot(!halted);
+      bool pred = true;
+      if (many(act)) {
+        Mask<W> goodS;
+        const bool good = sc.good_round(k, g.lane, a.R, goodS);
+        Mask<W> CB = mzero<W>(), CN = mzero<W>();
+        if (sc.crash_on) {
+          CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
+          CN = g.ballot(sc.crash_round == k);
+        }
+        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+        const Mask<W> Fl = mand(g.ballot(!(k <= maxR)), act);  // senders announcing their halt
+        const Mask<W> U = mor(M, H);                             // V = mailbox ++ halted.values
+        const int m = mpopc(U);
+        pred = !g.any(!halted && m < n - f);
+        // rank every process's current x in total order (ties by pid), scatter to LDS
+        const int64_t key = total_key(x);
+        int rank = 0;
+        if constexpr (W > 1) {
+          L.keys[g.pid] = key;
+          __syncthreads();
+        }
+        for (int j = 0; j < n; ++j) {
+          const int64_t kj = W == 1 ? (int64_t)readlane64((uint64_t)key, j) : L.keys[j];
+          rank += (kj < key || (kj == key && j < g.pid)) ? 1 : 0;
+        }
+        if (g.valid) {
+          sx[rank] = x;
+          spid[rank] = g.pid;
+        }
+        lds_sync<W>();
+        // walk the sorted values keeping the members of V: min, max, V(2f) and the
+        // trimmed every-2f-th sum (Epsilon.scala:31-42)
+        double first = 0.0, last = 0.0, e2f = 0.0, sum = 0.0;
+        int cnt = 0, j = 0;
+        for (int t = 0; t < n; ++t) {
+          const int q = spid[t];
+          if (mtest(U, q)) {
+            const double v = sx[t];
+            if (j == 0) first = v;
+            last = v;
+            if (j == 2 * f) e2f = v;
+            if (j >= f && j < m - f && (j - f) % (2 * f) == 0) {
+              sum += v;
+              ++cnt;
+            }
+            ++j;
+          }
+        }
+        if (!halted) {
+          H = mor(H, mand(M, Fl));  // halted ++ mailbox.filter(_._2._2)
+          if (k == 0) {
+            if (m > 0) {  // (empty V: Scala throws; left unchanged)
+              const double r1 = log((last - first) / eps) / logc;
+              maxR = d2i(ceil(r1));
+              if (a.variant == 1) maxR = 0;  // variant 1: mutation, no approximation rounds
+              if (m > 4 * f) x = e2f;  // reduce(2f, V).head
+            }
+          } else if (k <= maxR) {
+            x = sum / (double)cnt;  // sel.sum / sel.size (NaN for an empty sel)
+          } else {
+            decided = true;  // callback.decide(x); exitAtEndOfRound
+            decision = x;
+            dec_round = k;
+            halt_round = k;
+            halted = true;
+          }
+        }
+        lds_sync<W>();
+      }
+      eps_check<W>(g, ck, k + 1, full, decided, decision, eps, anyI, lo, hi, pred);
+    }
+    if (g.valid) {
+      const uint64_t off = i * (uint64_t)n + (uint64_t)g.pid;
+      if (a.out_dec_f64) a.out_dec_f64[off] = decided ? decision : 0.0;
+      if (a.out_rec_f64) {
+        a.out_rec_f64[2 * off] = decided ? decision : 0.0;
+        a.out_rec_f64[2 * off + 1] = x;
+      }
+    }
+    finish_instance<W>(g, a, i, ck, 3, decided ? fold32d(decision) : 0, dec_round, halt_round, fold32d(x), &bc);
+  }
+  __syncthreads();
+  counters_flush(&bc, a.counters, 3, a.R);
+}
+
+template <int W>
+static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(epsilon_kernel<W>, dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_epsilon(const KArgs& a, int W, int grid, hipStream_t s) {
+  switch (W) {
+    case 1: return launch_w<1>(a, grid, s);
+    case 2: return launch_w<2>(a, grid, s);
+    case 3: return launch_w<3>(a, grid, s);
+    case 4: return launch_w<4>(a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+const void* epsilon_kernel_ptr(int W) {
+  switch (W) {
+    case 1: return (const void*)epsilon_kernel<1>;
+    case 2: return (const void*)epsilon_kernel<2>;
+    case 3: return (const void*)epsilon_kernel<3>;
+    case 4: return (const void*)epsilon_kernel<4>;
+  }
+  return nullptr;
+}
+
+}  // namespace psg

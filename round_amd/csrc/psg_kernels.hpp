@@ -13,6 +13,7 @@ hipError_t launch_benor(const KArgs& a, int W, int grid, hipStream_t s);
 hipError_t launch_otr2(const KArgs& a, int W, int grid, hipStream_t s);
 hipError_t launch_slv(const KArgs& a, int W, int grid, hipStream_t s);
 hipError_t launch_kset_es(const KArgs& a, int W, int grid, hipStream_t s);
+hipError_t launch_epsilon(const KArgs& a, int W, int grid, hipStream_t s);
 
 const void* otr_kernel_ptr(int W);
 const void* lv_kernel_ptr(int W);
@@ -22,6 +23,7 @@ const void* benor_kernel_ptr(int W);
 const void* otr2_kernel_ptr(int W);
 const void* slv_kernel_ptr(int W);
 const void* kset_es_kernel_ptr(int W);
+const void* epsilon_kernel_ptr(int W);
 
 hipError_t launch_champ_selftest(const uint64_t* sets, int count, int tiebreak, int32_t* out, hipStream_t s);
 hipError_t launch_gen_init(uint64_t inst_begin, uint64_t count, int n, int alg, int V, uint64_t seed, int32_t* out,

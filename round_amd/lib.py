@@ -22,7 +22,7 @@ EXPORTED_SYMBOLS = [
     "psg_config_default", "psg_check_count", "psg_check_name", "psg_alg_from_class",
     "psg_create", "psg_load_inputs", "psg_run_batch", "psg_copy_decisions",
     "psg_fetch_instances", "psg_last_error", "psg_destroy", "psg_create_error",
-    "psg_selftest_map_head",
+    "psg_selftest_map_head", "psg_load_inputs_f64", "psg_copy_decisions_f64", "psg_fetch_instances_f64",
 ]
 
 
@@ -60,6 +60,11 @@ def load():
     L.psg_destroy.argtypes = [C.c_void_p]
     L.psg_destroy.restype = None
     L.psg_create_error.restype = C.c_char_p
+    L.psg_load_inputs_f64.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_double)]
+    L.psg_copy_decisions_f64.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
+    L.psg_fetch_instances_f64.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t,
+                                          C.POINTER(abi.InstanceSummary), C.POINTER(abi.ProcessRecord),
+                                          C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.psg_selftest_map_head.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
                                         C.POINTER(C.c_int32)]
     _lib = L
@@ -83,14 +88,24 @@ class Context:
         if rc != 0:
             raise PsgError(rc, load().psg_last_error(self._h).decode())
 
+    @property
+    def real(self):
+        return self.cfg.alg == abi.PSG_ALG_EPSILON
+
     def load_inputs(self, inst_begin, count, init=None):
         arr = None
         if init is not None:
-            flat = [int(v) for row in init for v in row]
+            if self.real:
+                flat = [float(v) for row in init for v in row]
+            else:
+                flat = [int(v) for row in init for v in row]
             if len(flat) != count * self.cfg.n:
                 raise ValueError("init must be [count][n]")
-            arr = (C.c_int32 * len(flat))(*flat)
-        self._check(load().psg_load_inputs(self._h, inst_begin, count, arr))
+            arr = ((C.c_double if self.real else C.c_int32) * len(flat))(*flat)
+        if self.real:
+            self._check(load().psg_load_inputs_f64(self._h, inst_begin, count, arr))
+        else:
+            self._check(load().psg_load_inputs(self._h, inst_begin, count, arr))
 
     def run_batch(self, inst_begin, count, per_instance=False):
         s = abi.Summary()
@@ -100,10 +115,16 @@ class Context:
         return s, (list(pi) if pi is not None else None)
 
     def copy_decisions(self):
+        """(decision, decision_round) of the last batch, [count*n] each (Double decisions
+        for real-valued algorithms)."""
         cells = self._last_count * self.cfg.n
-        dec = (C.c_int32 * cells)()
         dr = (C.c_int32 * cells)()
-        self._check(load().psg_copy_decisions(self._h, dec, dr))
+        if self.real:
+            dec = (C.c_double * cells)()
+            self._check(load().psg_copy_decisions_f64(self._h, dec, dr))
+        else:
+            dec = (C.c_int32 * cells)()
+            self._check(load().psg_copy_decisions(self._h, dec, dr))
         return list(dec), list(dr)
 
     def fetch(self, ids):
@@ -113,6 +134,17 @@ class Context:
         recs = (abi.ProcessRecord * (k * self.cfg.n))()
         self._check(load().psg_fetch_instances(self._h, arr, k, sums, recs))
         return list(sums), list(recs)
+
+    def fetch_real(self, ids):
+        """fetch() plus the Double decision and final x of every process ([k*n] each)."""
+        k = len(ids)
+        arr = (C.c_uint64 * k)(*ids)
+        sums = (abi.InstanceSummary * k)()
+        recs = (abi.ProcessRecord * (k * self.cfg.n))()
+        dec = (C.c_double * (k * self.cfg.n))()
+        fx = (C.c_double * (k * self.cfg.n))()
+        self._check(load().psg_fetch_instances_f64(self._h, arr, k, sums, recs, dec, fx))
+        return list(sums), list(recs), list(dec), list(fx)
 
     def close(self):
         if getattr(self, "_h", None):

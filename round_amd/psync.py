@@ -56,6 +56,8 @@ class Algorithm:
     class_name = ""
     alg_id = 0
     phase_length = 1  # rounds.length (psync/Process.scala:28)
+    real = False  # Double-valued (RealConsensusIO) algorithm
+    epsilon = 0.0
 
     def __init__(self, param=0, variant=0, param2=0):
         self.param = int(param)
@@ -198,8 +200,27 @@ class KSetEarlyStopping(Algorithm):
         return 1_000_000
 
 
+class EpsilonConsensus(Algorithm):
+    """example.EpsilonConsensus(rt, f, epsilon, timeout) — example/Epsilon.scala:72 (Double
+    values; runner defaults f = 1, epsilon = 0.1, 7 replicas, Epsilon.scala:83-89)."""
+    class_name = "example.EpsilonConsensus"
+    alg_id = abi.PSG_ALG_EPSILON
+    real = True
+
+    def __init__(self, f=1, epsilon=0.1, variant=0):
+        super().__init__(f, variant)
+        self.epsilon = float(epsilon)
+
+    def default_schedule(self, n):
+        # |mailbox| >= n - f (the commented assert, Epsilon.scala:57): HO(p) := all below that
+        return HOSchedule(drop_log2=4, good_round=0.0, ho_min=n - self.param - 1)
+
+    def default_rounds(self, n):
+        return 12
+
+
 ALGORITHMS = {c.class_name: c for c in (OTR, LastVoting, FloodMin, KSetAgreement, BenOr,
-                                          OTR2, ShortLastVoting, KSetEarlyStopping)}
+                                          OTR2, ShortLastVoting, KSetEarlyStopping, EpsilonConsensus)}
 
 
 def make_config(alg: Algorithm, n: int, rounds: Optional[int] = None, seed: int = 1,
@@ -220,6 +241,7 @@ def make_config(alg: Algorithm, n: int, rounds: Optional[int] = None, seed: int 
     c.value_range = alg.default_value_range(n) if value_range is None else value_range
     c.param = alg.param
     c.param2 = alg.param2
+    c.real_param = alg.epsilon
     c.tiebreak = tiebreak
     c.device = device
     c.variant = alg.variant
@@ -282,6 +304,9 @@ class GpuRound:
 
     def fetch(self, ids: Sequence[int]):
         return self._ctx.fetch(ids)
+
+    def fetch_real(self, ids: Sequence[int]):
+        return self._ctx.fetch_real(ids)
 
     def close(self):
         if self._ctx is not None:

@@ -43,6 +43,8 @@ FIXTURES = {
     "w2_slv_n16_loss": (psync.ShortLastVoting(), 16, 400, dict(value_range=5, seed=7, schedule=H(
         drop_log2=1, good_round=0.0, crash_fmax=7))),
     "w2_kset_es_n64_t8_k2": (psync.KSetEarlyStopping(8, 2), 64, 200, dict(seed=8)),
+    "w2_epsilon_n7_f1": (psync.EpsilonConsensus(1, 0.1), 7, 300, dict(seed=9)),
+    "w2_epsilon_n64_f5": (psync.EpsilonConsensus(5, 1e-6), 64, 100, dict(seed=9)),
 }
 
 BEGIN = 12345
@@ -72,8 +74,15 @@ def inst_row(s):
 def make(name):
     alg, n, count, kw = FIXTURES[name]
     cfg = psync.make_config(alg, n, batch_capacity=count, **kw)
-    s, pi, rec = oracle.run(cfg, BEGIN, count, per_instance=True, records=True, threads=8)
-    return {
+    extra = {}
+    if alg.real:
+        s, pi, rec, dec, fx = oracle.run_real(cfg, BEGIN, count, per_instance=True, records=True, threads=8)
+        # Double decision / final x (JSON floats round-trip exactly)
+        extra["records_f64"] = {str(BEGIN + i): [[dec[i * n + p], fx[i * n + p]] for p in range(n)]
+                                for i in range(N_RECORDS)}
+    else:
+        s, pi, rec = oracle.run(cfg, BEGIN, count, per_instance=True, records=True, threads=8)
+    return dict(extra, **{
         "name": name,
         "class": alg.class_name,
         "config": config_dict(cfg),
@@ -89,7 +98,7 @@ def make(name):
         "instances": [inst_row(x) for x in pi],
         "records": {str(BEGIN + i): [[r.decision, r.decision_round, r.halt_round, r.final_x]
                                      for r in rec[i * n:(i + 1) * n]] for i in range(N_RECORDS)},
-    }
+    })
 
 
 def main():

@@ -17,7 +17,7 @@ HEADER = os.path.join(ROOT, "include", "psg.h")
 def header_functions():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(psg_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(psg_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -44,6 +44,7 @@ int main(void) {
   printf("psg_instance_summary %zu\n", sizeof(psg_instance_summary));
   printf("psg_process_record %zu\n", sizeof(psg_process_record));
   P(psg_config, seed) P(psg_config, value_range) P(psg_config, batch_capacity) P(psg_config, sched)
+  P(psg_config, param2) P(psg_config, real_param)
   P(psg_summary, fail_count) P(psg_summary, decided_processes) P(psg_summary, term_hist) P(psg_summary, kernel_ns)
   P(psg_instance_summary, first_fail) P(psg_instance_summary, term_round) P(psg_instance_summary, n_decided)
   P(psg_schedule, crash_fmax) P(psg_schedule, self_bit)
@@ -68,6 +69,8 @@ def test_struct_layouts_match_header(tmp_path):
         "psg_config.value_range": abi.Config.value_range.offset,
         "psg_config.batch_capacity": abi.Config.batch_capacity.offset,
         "psg_config.sched": abi.Config.sched.offset,
+        "psg_config.param2": abi.Config.param2.offset,
+        "psg_config.real_param": abi.Config.real_param.offset,
         "psg_summary.fail_count": abi.Summary.fail_count.offset,
         "psg_summary.decided_processes": abi.Summary.decided_processes.offset,
         "psg_summary.term_hist": abi.Summary.term_hist.offset,

@@ -186,3 +186,81 @@ def test_gpu_map_head_matches_oracle(oracle_mod):
             pids = [q for q in range(64) if (m >> q) & 1]
             want = oracle_mod.scala_map_order(pids, tb)[0] if pids else -1
             assert h == want, (hex(m), tb, h, want)
+
+
+# --------------------------------------------------------------------------- EpsilonConsensus (Double)
+# Values: every step is the same IEEE operation in the same order on both sides, so
+# the GPU reproduces the oracle bit for bit; the stated tolerance covers libm log()
+# differing by an ulp (which can move maxR only when r1 sits within an ulp of an
+# integer). Integer results (rounds, first failing check points) must match exactly.
+F64_ABS_TOL = 1e-12
+
+EPS_CASES = [
+    ("eps-n7-f1", psync.EpsilonConsensus(1, 0.1), 7, 4000, dict(seed=60)),
+    ("eps-n16-f2", psync.EpsilonConsensus(2, 1e-3), 16, 2000, dict(seed=61)),
+    ("eps-n64-f5", psync.EpsilonConsensus(5, 1e-6), 64, 1000, dict(seed=62)),
+    ("eps-n64-loss-nan", psync.EpsilonConsensus(3, 1e-3), 64, 1000, dict(seed=63, schedule=psync.HOSchedule(
+        drop_log2=1, good_round=0.0))),
+    ("eps-n7-pureho", psync.EpsilonConsensus(1, 0.05), 7, 3000, dict(seed=64, schedule=psync.HOSchedule(
+        drop_log2=2, good_round=0.0, self_bit=False))),
+    ("eps-n40-crash", psync.EpsilonConsensus(4, 1e-4), 40, 1000, dict(seed=65, schedule=psync.HOSchedule(
+        drop_log2=3, good_round=0.0, crash_fmax=4))),
+    ("eps-mutant-n7", psync.EpsilonConsensus(1, 0.01, variant=1), 7, 3000, dict(seed=66, schedule=psync.HOSchedule(
+        drop_log2=2, good_round=0.0, ho_min=5))),
+    ("eps-n100-W2", psync.EpsilonConsensus(10, 1e-5), 100, 300, dict(seed=67, rounds=16)),
+    ("eps-n256-W4", psync.EpsilonConsensus(40, 1e-3), 256, 60, dict(seed=68, rounds=16)),
+]
+
+
+def _close(a, b, tol=F64_ABS_TOL):
+    import math
+    if math.isnan(a) or math.isnan(b):
+        return math.isnan(a) and math.isnan(b)
+    return abs(a - b) <= tol
+
+
+def _check_eps(gr, res, dec, dround, begin, count, init=None, oracle_mod=None):
+    n = gr.cfg.n
+    osum, opi, orec, odec, ofx = oracle_mod.run_real(gr.cfg, begin, count, init=init, per_instance=True,
+                                                     records=True, threads=8)
+    _cmp_summary(res.summary, osum, gr.cfg.rounds)
+    for i in range(count):
+        g, o = res.per_instance[i], opi[i]
+        assert (tuple(g.first_fail), g.term_round, g.n_decided) == (tuple(o.first_fail), o.term_round, o.n_decided), i
+        assert g.digest == o.digest, i
+    for c in range(count * n):
+        assert dround[c] == orec[c].decision_round, c
+        assert _close(dec[c], odec[c]), (c, dec[c], odec[c])
+    return opi, orec, odec, ofx
+
+
+@pytest.mark.parametrize("cid,alg,n,count,kw", EPS_CASES, ids=[c[0] for c in EPS_CASES])
+def test_gpu_epsilon_matches_oracle(cid, alg, n, count, kw, oracle_mod):
+    begin = 777
+    with psync.GpuRound(alg, n, batch_capacity=count, **kw) as gr:
+        res = gr.run(begin, count, per_instance=True)
+        dec, dround = gr.decisions()
+        sample = [begin + i for i in range(0, count, max(1, count // 23))]
+        fsums, frecs, fdec, ffx = gr.fetch_real(sample)
+    opi, orec, odec, ofx = _check_eps(gr, res, dec, dround, begin, count, oracle_mod=oracle_mod)
+    for j, inst in enumerate(sample):
+        i = inst - begin
+        assert _inst_tuple(fsums[j]) == _inst_tuple(opi[i])
+        for p in range(n):
+            assert _rec_tuple(frecs[j * n + p]) == _rec_tuple(orec[i * n + p]), (inst, p)
+            assert _close(fdec[j * n + p], odec[i * n + p]) and _close(ffx[j * n + p], ofx[i * n + p]), (inst, p)
+
+
+def test_gpu_epsilon_host_inputs(oracle_mod):
+    """psg_load_inputs_f64: caller Doubles incl. negatives, -0.0 / 0.0, duplicates and NaN."""
+    import random
+    rng = random.Random(9)
+    n, count = 16, 400
+    pool = [0.0, -0.0, 1.0, -1.0, 0.5, 0.5, 1e-300, -1e300, float("nan")]
+    init = [[rng.choice(pool) if rng.random() < 0.3 else rng.uniform(-5, 5) for _ in range(n)]
+            for _ in range(count)]
+    with psync.GpuRound(psync.EpsilonConsensus(2, 1e-3), n, seed=70, batch_capacity=count) as gr:
+        gr.load_inputs(5, count, init)
+        res = gr.run(5, count, per_instance=True)
+        dec, dround = gr.decisions()
+    _check_eps(gr, res, dec, dround, 5, count, init=init, oracle_mod=oracle_mod)

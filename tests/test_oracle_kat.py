@@ -257,6 +257,35 @@ def test_short_last_voting_maxby_champ_order(oracle_mod):
     assert all(r.decision == init[first] and r.decision_round == 2 for r in rec)
 
 
+def test_epsilon_rounds_and_trimmed_mean(oracle_mod):
+    """n = 7, f = 1, epsilon = 0.1, all HO full, init 0.0 .. 0.6: round 0 diff = 0.6,
+    c(n-3f, 2f) = (4-1)/2 + 1 = 2, maxR = ceil(log(6)/log(2)) = 3, x = sorted V(2f) = 0.2;
+    rounds 1..3 average every 2nd of the 5 trimmed copies of x; round 4 (> maxR)
+    decides and exits."""
+    cfg = cfg_for(psync.EpsilonConsensus(1, 0.1), 7, 6)
+    init = [0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6]
+    s, rec, dec, fx = oracle_mod.run_explicit_real(cfg, init, [[0x7F] * 7] * 6)
+    x = 0.2
+    for _ in range(3):
+        x = (x + x + x) / 3  # sel = red(0), red(2), red(4), left fold from 0.0
+    assert [(r.decision_round, r.halt_round) for r in rec] == [(4, 4)] * 7
+    assert dec == [x] * 7 and fx == [x] * 7
+    assert list(s.first_fail)[:3] == [NEVER] * 3 and s.term_round == 5
+
+
+def test_epsilon_halted_values_are_remembered(oracle_mod):
+    """p6 hears only itself in round 0 (V = {0.6}: diff 0 -> log(0) = -inf -> maxR =
+    Int.MinValue, x unchanged since |V| <= 4f), so it announces its halt in round 1
+    and exits; the others keep its 0.6 in `halted` and still see 7 values in round 2."""
+    cfg = cfg_for(psync.EpsilonConsensus(1, 0.1), 7, 6)
+    init = [0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6]
+    r0 = [0x7F] * 6 + [0x40]
+    s, rec, dec, fx = oracle_mod.run_explicit_real(cfg, init, [r0] + [[0x7F] * 7] * 5)
+    assert (rec[6].decision_round, rec[6].halt_round) == (1, 1) and dec[6] == 0.6
+    assert s.first_fail[2] == NEVER or s.first_fail[2] > 0  # |V| >= n - f is not broken by the halt
+    assert all(r.decision_round == 4 for r in rec[:6])
+
+
 # --------------------------------------------------------------------------- third-party algorithms
 def test_philox_known_answers(oracle_mod):
     """Random123 kat_vectors, philox4x32 R=10."""

@@ -61,6 +61,31 @@ def test_zero_false_positives(alg, n, kw, oracle_mod):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("alg,n,kw", [
+    (psync.EpsilonConsensus(1, 0.1), 7, {}),
+    (psync.EpsilonConsensus(2, 1e-3), 16, {}),
+    (psync.EpsilonConsensus(5, 1e-6), 64, {}),
+    (psync.EpsilonConsensus(1, 0.1), 7, dict(schedule=H(drop_log2=1, good_round=0.0))),
+])
+def test_epsilon_violations_only_after_safety_predicate_breaks(alg, n, kw, oracle_mod):
+    """Approximate agreement / validity hold in every instance whose processes always had
+    |V| >= n - f values (Epsilon.scala:57); with heavy loss the assumption breaks and
+    violations appear only after it has."""
+    cfg = psync.make_config(alg, n, seed=33, **kw)
+    _, pi, _, _, _ = oracle_mod.run_real(cfg, 0, 1500, per_instance=True, threads=8)
+    for s in pi:
+        for slot in (0, 1):
+            if s.first_fail[slot] != NEVER:
+                assert s.first_fail[2] != NEVER and s.first_fail[2] <= s.first_fail[slot]
+
+
+def test_epsilon_mutant_is_caught(oracle_mod):
+    cfg = psync.make_config(psync.EpsilonConsensus(1, 0.01, variant=1), 7, seed=34,
+                            schedule=H(drop_log2=2, good_round=0.0, ho_min=5))
+    s, pi, _, _, _ = oracle_mod.run_real(cfg, 0, 2000, per_instance=True, threads=8)
+    assert sum(1 for x in pi if x.first_fail[0] != NEVER and x.first_fail[2] == NEVER) > 0
+
+
 @pytest.mark.parametrize("n", [4, 8, 16])
 def test_benor_violations_only_after_safety_predicate_breaks(n, oracle_mod):
     """BenOr's invariant assumes |HO(p)| > n/2 (BenOr.scala:272). Deciders exit, so
