@@ -4,10 +4,11 @@
   C3  LastVoting n=64, 1e8 instances over 8 GPUs (1.25e7 per GPU), 20 rounds, crash-stop
   C4  FloodMin n=256 crash-stop sweep f in {0,1,2,4,...,64}, R = f+2; KSetAgreement n=256, k=2, R=16
   C5  BenOr n=128, 64 rounds, |HO(p)| > n/2; termination-round histogram all-reduced
+  W2  second-wave algorithms: OTR2, ShortLastVoting, KSetEarlyStopping, EpsilonConsensus
 
 One process per GPU (torchrun), weak scaling, RCCL all-reduce of the summaries.
 Prints one JSON line per configuration (rank 0). Algorithmic bytes per
-process-round per SURVEY §8d: OTR 24, LV 42, FloodMin 8, KSet 70, BenOr 11.
+process-round per SURVEY §8d: OTR 24, LV 42, FloodMin 8, KSet 70, BenOr 11 (W2 rows below).
 """
 import argparse
 import json
@@ -35,6 +36,15 @@ def configs(scale):
         out.append((f"C4_floodmin_n256_f{f}", psync.FloodMin(f), 256, int(1_000_000 * s), {}, 8))
     out.append(("C4_kset_n256_k2", psync.KSetAgreement(2), 256, int(200_000 * s), {}, 70))
     out.append(("C5_benor_n128", psync.BenOr(), 128, int(1_000_000 * s), {}, 11))
+    # second-wave algorithms (not BASELINE configurations). B_alg by the
+    # §8d recipe: (state read + written) + init. OTR2 = OTR; SLV (x, ts, vote, decision 4 B
+    # + commit, decided 1 B) x 2 + 4; KSetEarlyStopping (est, lastNb, decision 4 B + canDecide,
+    # decided 1 B) x 2 + 4; Epsilon n=64 (x, decision 8 B + maxR 4 B + halted-set 8 B +
+    # decided 1 B) x 2 + init 8.
+    out.append(("W2_otr2_n64", psync.OTR2(), 64, int(10_000_000 * s), dict(value_range=64), 24))
+    out.append(("W2_slv_n64", psync.ShortLastVoting(), 64, int(12_500_000 * s), {}, 40))
+    out.append(("W2_kset_es_n256_t64_k2", psync.KSetEarlyStopping(64, 2), 256, int(1_000_000 * s), {}, 32))
+    out.append(("W2_epsilon_n64_f5", psync.EpsilonConsensus(5, 1e-6), 64, int(1_000_000 * s), {}, 66))
     return out
 
 
