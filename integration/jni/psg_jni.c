@@ -29,13 +29,13 @@ static void throw_psg(JNIEnv* env, int rc, const char* msg) {
   if (ex) (*env)->ThrowNew(env, ex, buf);
 }
 
-/* long create(int alg, int n, int rounds, long seed, int valueRange, int param, int tiebreak,
- *             int device, int variant, long batchCapacity,
+/* long create(int alg, int n, int rounds, long seed, int valueRange, int param, int param2, double realParam,
+ *             int tiebreak, int device, int variant, long batchCapacity,
  *             int dropLog2, int goodP32, int goodMin, int crashFmax, int hoMin, boolean selfBit) */
 JNIEXPORT jlong JNICALL Java_psync_gpu_GpuRoundNative_00024_create(
-    JNIEnv* env, jobject self, jint alg, jint n, jint rounds, jlong seed, jint valueRange, jint param, jint tiebreak,
-    jint device, jint variant, jlong batchCapacity, jint dropLog2, jint goodP32, jint goodMin, jint crashFmax,
-    jint hoMin, jboolean selfBit) {
+    JNIEnv* env, jobject self, jint alg, jint n, jint rounds, jlong seed, jint valueRange, jint param, jint param2,
+    jdouble realParam, jint tiebreak, jint device, jint variant, jlong batchCapacity, jint dropLog2, jint goodP32,
+    jint goodMin, jint crashFmax, jint hoMin, jboolean selfBit) {
   (void)self;
   psg_config c;
   memset(&c, 0, sizeof c);
@@ -46,6 +46,8 @@ JNIEXPORT jlong JNICALL Java_psync_gpu_GpuRoundNative_00024_create(
   c.seed = (uint64_t)seed;
   c.value_range = valueRange;
   c.param = param;
+  c.param2 = param2;
+  c.real_param = realParam;
   c.tiebreak = tiebreak;
   c.device = device;
   c.variant = variant;
@@ -139,6 +141,30 @@ JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_fetch(JNIEnv* env, jo
   (*env)->ReleaseLongArrayElements(env, ids, id, JNI_ABORT);
   if (rc == 0) (*env)->SetByteArrayRegion(env, sums, 0, (jsize)(sizeof(*s) * (size_t)k), (const jbyte*)s);
   free(s);
+  if (rc) throw_psg(env, rc, psg_last_error(ctx));
+}
+
+/* void loadInputsF64(long ctx, long begin, long count, double[] init) — RealConsensusIO inputs */
+JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_loadInputsF64(JNIEnv* env, jobject self, jlong h,
+                                                                         jlong begin, jlong count, jdoubleArray init) {
+  (void)self;
+  psg_ctx* ctx = (psg_ctx*)(intptr_t)h;
+  jdouble* p = init ? (*env)->GetDoubleArrayElements(env, init, NULL) : NULL;
+  int rc = psg_load_inputs_f64(ctx, (uint64_t)begin, (uint64_t)count, (const double*)p);
+  if (p) (*env)->ReleaseDoubleArrayElements(env, init, p, JNI_ABORT);
+  if (rc) throw_psg(env, rc, psg_last_error(ctx));
+}
+
+/* void copyDecisionsF64(long ctx, double[] decision, int[] round) — RealConsensusIO.decide values */
+JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_copyDecisionsF64(JNIEnv* env, jobject self, jlong h,
+                                                                            jdoubleArray dec, jintArray round) {
+  (void)self;
+  psg_ctx* ctx = (psg_ctx*)(intptr_t)h;
+  jdouble* d = (*env)->GetDoubleArrayElements(env, dec, NULL);
+  jint* r = (*env)->GetIntArrayElements(env, round, NULL);
+  int rc = psg_copy_decisions_f64(ctx, (double*)d, (int32_t*)r);
+  (*env)->ReleaseDoubleArrayElements(env, dec, d, 0);
+  (*env)->ReleaseIntArrayElements(env, round, r, 0);
   if (rc) throw_psg(env, rc, psg_last_error(ctx));
 }
 

@@ -15,10 +15,12 @@ import psync.Algorithm
 /** JNI entry points (one per psg.h function). */
 object GpuRoundNative {
   System.loadLibrary("psg_jni")
-  @native def create(alg: Int, n: Int, rounds: Int, seed: Long, valueRange: Int, param: Int, tiebreak: Int,
-                     device: Int, variant: Int, batchCapacity: Long, dropLog2: Int, goodP32: Int, goodMin: Int,
-                     crashFmax: Int, hoMin: Int, selfBit: Boolean): Long
+  @native def create(alg: Int, n: Int, rounds: Int, seed: Long, valueRange: Int, param: Int, param2: Int,
+                     realParam: Double, tiebreak: Int, device: Int, variant: Int, batchCapacity: Long, dropLog2: Int,
+                     goodP32: Int, goodMin: Int, crashFmax: Int, hoMin: Int, selfBit: Boolean): Long
   @native def loadInputs(ctx: Long, begin: Long, count: Long, init: Array[Int]): Unit
+  @native def loadInputsF64(ctx: Long, begin: Long, count: Long, init: Array[Double]): Unit
+  @native def copyDecisionsF64(ctx: Long, decision: Array[Double], decisionRound: Array[Int]): Unit
   @native def runBatch(ctx: Long, begin: Long, count: Long, perInstance: Array[Byte]): Array[Long]
   @native def copyDecisions(ctx: Long, decision: Array[Int], decisionRound: Array[Int]): Unit
   @native def fetch(ctx: Long, ids: Array[Long], sums: Array[Byte], records: Array[Int]): Unit
@@ -29,9 +31,12 @@ object GpuRoundNative {
 case class HOSchedule(dropLog2: Int = 3, goodRound: Double = 0.25, goodMin: Int = -1,
                       crashFmax: Int = -1, hoMin: Int = -1, selfBit: Boolean = true)
 
+/** param: OTR/OTR2 afterDecision, FloodMin f, KSet k, KSetEarlyStopping t, EpsilonConsensus f;
+  * param2: KSetEarlyStopping k; realParam: EpsilonConsensus epsilon. */
 case class GpuConfig(n: Int, rounds: Int, seed: Long = 1L, valueRange: Int = 4, param: Int = 0,
                      schedule: HOSchedule = HOSchedule(), tiebreakChamp: Boolean = true,
-                     device: Int = 0, batchCapacity: Long = 1L << 20, variant: Int = 0)
+                     device: Int = 0, batchCapacity: Long = 1L << 20, variant: Int = 0,
+                     param2: Int = 0, realParam: Double = 0.0)
 
 /** Node-level result of a batch (psg_summary). */
 case class GpuResult(instances: Long, processRounds: Long, failCount: Array[Long], decidedProcesses: Long,
@@ -41,7 +46,9 @@ object GpuRound {
   /** Algorithm ids keyed on the reference class (SURVEY §8b). */
   val registry: Map[String, Int] = Map(
     "example.OTR" -> 1, "example.LastVoting" -> 2, "example.FloodMin" -> 3,
-    "example.KSetAgreement" -> 4, "example.BenOr" -> 5)
+    "example.KSetAgreement" -> 4, "example.BenOr" -> 5, "example.OTR2" -> 6,
+    "example.ShortLastVoting" -> 7, "example.KSetEarlyStopping" -> 8, "example.EpsilonConsensus" -> 9)
+  private val realValued = Set(9)
 
   def algId(alg: Algorithm[_, _]): Int =
     registry.getOrElse(alg.getClass.getName,
@@ -56,12 +63,43 @@ object GpuRound {
   /** Run instances [begin, begin+count) of `alg` in lockstep on one GPU. `init`
     * (optional, count*n) plays ConsensusIO.initialValue; `decide` receives the
     * ConsensusIO.decide callbacks (instance, pid, value, round) afterwards. */
-  def run(alg: Algorithm[_, _], cfg: GpuConfig, begin: Long, count: Long, init: Option[Array[Int]] = None,
-          decide: Option[(Long, Int, Int, Int) => Unit] = None): GpuResult = {
+  private def create(id: Int, cfg: GpuConfig): Long = {
     val s = cfg.schedule
-    val ctx = GpuRoundNative.create(algId(alg), cfg.n, cfg.rounds, cfg.seed, cfg.valueRange, cfg.param,
+    GpuRoundNative.create(id, cfg.n, cfg.rounds, cfg.seed, cfg.valueRange, cfg.param, cfg.param2, cfg.realParam,
       if (cfg.tiebreakChamp) 0 else 1, cfg.device, cfg.variant, cfg.batchCapacity, s.dropLog2,
       math.min(s.goodRound * 4294967296.0, 4294967295.0).toLong.toInt, s.goodMin, s.crashFmax, s.hoMin, s.selfBit)
+  }
+
+  /** RealConsensusIO algorithms (EpsilonConsensus, example/Epsilon.scala:10-13): Double
+    * initial values and decide callbacks. */
+  def runReal(alg: Algorithm[_, _], cfg: GpuConfig, begin: Long, count: Long, init: Option[Array[Double]] = None,
+              decide: Option[(Long, Int, Double, Int) => Unit] = None): GpuResult = {
+    val id = algId(alg)
+    if (!realValued(id)) throw new IllegalArgumentException(alg.getClass.getName + " is not real-valued")
+    val ctx = create(id, cfg)
+    try {
+      GpuRoundNative.loadInputsF64(ctx, begin, count, init.orNull)
+      val res = summary(GpuRoundNative.runBatch(ctx, begin, count, null), cfg.rounds)
+      decide.foreach { cb =>
+        val cells = (count * cfg.n).toInt
+        val d = new Array[Double](cells)
+        val r = new Array[Int](cells)
+        GpuRoundNative.copyDecisionsF64(ctx, d, r)
+        var i = 0
+        while (i < cells) {
+          if (r(i) >= 0) cb(begin + i / cfg.n, i % cfg.n, d(i), r(i))
+          i += 1
+        }
+      }
+      res
+    } finally GpuRoundNative.destroy(ctx)
+  }
+
+  def run(alg: Algorithm[_, _], cfg: GpuConfig, begin: Long, count: Long, init: Option[Array[Int]] = None,
+          decide: Option[(Long, Int, Int, Int) => Unit] = None): GpuResult = {
+    val id = algId(alg)
+    if (realValued(id)) throw new IllegalArgumentException(alg.getClass.getName + " is real-valued: use runReal")
+    val ctx = create(id, cfg)
     try {
       GpuRoundNative.loadInputs(ctx, begin, count, init.orNull)
       val res = summary(GpuRoundNative.runBatch(ctx, begin, count, null), cfg.rounds)
