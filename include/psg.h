@@ -153,6 +153,77 @@ typedef struct psg_process_record {
   int32_t final_x;        /* final main variable (OTR/LV/FloodMin x, BenOr x, KSet pick(t)) */
 } psg_process_record;
 
+/* ---------------------------------------------------------------------------
+ * Generic Spec evaluation: a Spec given as a compiled
+ * Formula program instead of the algorithm's hand-lowered checks.
+ *
+ * Replaces, for concrete checking, the Spec / Formula surface of the reference
+ * (psync/Specs.scala:8-16, psync/formula/Formula.scala: ForAll / Exists /
+ * Comprehension / Cardinality / Literal / Variable / Application; the `init` /
+ * `old` wrappers and Option isDefined / get of psync/macros/FormulaExtractor.scala).
+ * The host compiler (round_amd/formula.py) turns a Formula tree into this
+ * stack bytecode; the device evaluates it after every round over a trace of the
+ * process states. Quantified process variables range over the pids 0..n-1,
+ * V.exists over Int is finitized exactly (candidate values compared with the
+ * variable, +-1, plus Int.MinValue / Int.MaxValue).
+ * ------------------------------------------------------------------------- */
+
+/* Process-state fields visible to a Spec (the variables the reference specs read). */
+enum psg_field {
+  PSG_FIELD_X = 0,        /* x (OTR/LV/FloodMin/SLV), est (KSetEarlyStopping), pick(t) (KSet), x (BenOr 0/1) */
+  PSG_FIELD_DECIDED = 1,  /* decided flag (ghost for algorithms without one: decide callback fired) */
+  PSG_FIELD_DECISION = 2, /* decision (OTR2: Option, PSG_NONE32 when empty) */
+  PSG_FIELD_TS = 3,       /* LastVoting / ShortLastVoting ts */
+  PSG_FIELD_READY = 4,    /* LastVoting ready */
+  PSG_FIELD_COMMIT = 5,   /* LastVoting / ShortLastVoting commit */
+  PSG_FIELD_VOTE = 6,     /* LastVoting / SLV vote; BenOr vote (Option[Boolean], PSG_NONE32 when empty) */
+  PSG_FIELD_CANDECIDE = 7,/* BenOr canDecide */
+  PSG_FIELD_HOSIZE = 8,   /* |mailbox| of the round just executed (n if the process took no step) */
+  PSG_NFIELDS = 9
+};
+/* Which state a field is read from (FormulaExtractor init(...) / old(...)). */
+enum psg_tag { PSG_TAG_CUR = 0, PSG_TAG_OLD = 1, PSG_TAG_INIT = 2 };
+#define PSG_NONE32 ((int32_t)0x80000000) /* Option None in an int32 field */
+
+/* Bytecode: word = op | a << 8 | b << 16 (b signed 16-bit). Per-lane int32 stack. */
+enum psg_op {
+  PSG_OP_HALT = 0,   /* end of an expression: result = top of stack */
+  PSG_OP_IMM = 1,    /* push b */
+  PSG_OP_IMM32 = 2,  /* push the next code word */
+  PSG_OP_N = 3,      /* push n */
+  PSG_OP_R = 4,      /* push r (check point: completed rounds) */
+  PSG_OP_VAR = 5,    /* push bound variable a */
+  PSG_OP_FIELD = 6,  /* p = pop; push field a (enum psg_field) of process p in state b (enum psg_tag) */
+  PSG_OP_NOT = 7, PSG_OP_NEG = 8, PSG_OP_ISDEF = 9, /* ISDEF: v != PSG_NONE32 */
+  PSG_OP_AND = 10, PSG_OP_OR = 11, PSG_OP_IMPL = 12,
+  PSG_OP_EQ = 13, PSG_OP_NE = 14, PSG_OP_LT = 15, PSG_OP_LE = 16, PSG_OP_GT = 17, PSG_OP_GE = 18,
+  PSG_OP_ADD = 19, PSG_OP_SUB = 20, PSG_OP_MUL = 21,
+  PSG_OP_DIV = 22, PSG_OP_MOD = 23, /* Scala Int semantics (truncation); x / 0 and x % 0 evaluate to 0 */
+  PSG_OP_BIND = 24,  /* bound variable a = pop (Set.contains(e) of a comprehension) */
+  PSG_OP_QBEGIN = 25,/* quantifier kind a over bound variable b; next word: pc of the matching QEND;
+                        EXISTS_VI: then one word = (#expression candidates popped from the stack) | (#field
+                        sets) << 16, then one word per field set = field | tag << 8 */
+  PSG_OP_QEND = 26,
+  PSG_OP_COORD = 27  /* push (r / 4) % n (LastVoting / ShortLastVoting coord(r/4)) */
+};
+enum psg_quant {
+  PSG_Q_FORALL_P = 0, PSG_Q_EXISTS_P = 1, PSG_Q_COUNT_P = 2,    /* over pids, one at a time */
+  PSG_Q_FORALL_PL = 3, PSG_Q_EXISTS_PL = 4, PSG_Q_COUNT_PL = 5, /* over pids, one lane per pid (not nested) */
+  PSG_Q_EXISTS_VB = 6,                                          /* V.exists over Boolean */
+  PSG_Q_EXISTS_VI = 7                                           /* V.exists over Int (finitized) */
+};
+#define PSG_SPEC_RELATIONAL 1 /* slot flag: reads old(...), vacuously true at check point 0 */
+
+typedef struct psg_spec_program {
+  int32_t n_slots;           /* check slots, 1..PSG_MAX_CHECKS */
+  int32_t n_words;           /* code length */
+  const int32_t* code;       /* bytecode */
+  const int32_t* slot_entry; /* [n_slots] pc of each slot's expression (ends in PSG_OP_HALT) */
+  const int32_t* slot_flags; /* [n_slots] PSG_SPEC_* */
+  int32_t term_entry;        /* pc of the Termination expression, -1 for none */
+  int32_t n_vars;            /* bound variables used, <= 16 */
+} psg_spec_program;
+
 typedef struct psg_ctx psg_ctx;
 
 /* Fill *cfg with the defaults for algorithm alg at n processes. */
@@ -188,6 +259,15 @@ int psg_copy_decisions(psg_ctx* ctx, int32_t* decision, int32_t* decision_round)
  * summaries (k entries) and per-process records (k * n entries, nullable). */
 int psg_fetch_instances(psg_ctx* ctx, const uint64_t* ids, size_t k,
                         psg_instance_summary* sums, psg_process_record* procs);
+
+/* Like psg_run_batch, but the Spec is the given program: fail_count / term_hist /
+ * first_fail / term_round come from it (digest, decisions, records from the
+ * round execution as usual). Integer-state algorithms only (not EpsilonConsensus).
+ * The process states of every check point are traced in HBM and evaluated by the
+ * device interpreter; large batches are processed in chunks of at most
+ * PSG_SPEC_TRACE_MB (environment, default 2048) MiB of trace. */
+int psg_run_batch_spec(psg_ctx* ctx, uint64_t inst_begin, uint64_t inst_count, const psg_spec_program* prog,
+                       psg_summary* out, psg_instance_summary* per_inst);
 
 /* Real-valued algorithms (PSG_ALG_EPSILON, RealConsensusIO, Epsilon.scala:10-13).
  * Same contracts as the int32 entry points; other algorithms get PSG_EINVAL.

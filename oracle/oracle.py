@@ -52,6 +52,12 @@ def lib():
                                                C.POINTER(abi.InstanceSummary), C.POINTER(abi.ProcessRecord),
                                                C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.oracle_run_explicit_real.restype = C.c_int
+        L.oracle_trace.argtypes = [C.POINTER(abi.Config), C.c_uint64, C.c_uint64, C.POINTER(C.c_int32),
+                                   C.POINTER(C.c_int32), C.c_int32]
+        L.oracle_trace.restype = C.c_int
+        L.oracle_vm_run.argtypes = [C.POINTER(abi.SpecProgram), C.POINTER(C.c_int32), C.c_uint64, C.c_int32,
+                                    C.c_int32, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]
+        L.oracle_vm_run.restype = C.c_int
         L.oracle_last_error.restype = C.c_char_p
         L.oracle_philox.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.oracle_java_first_boolean.argtypes = [C.c_int64]
@@ -202,3 +208,31 @@ def init_value(cfg, inst, p):
 
 def crash_round(cfg, inst, p):
     return lib().oracle_crash_round(C.byref(cfg), inst, p)
+
+
+NFIELDS = 9
+
+
+def trace(cfg, inst_begin, count, init=None, threads=8):
+    """Per-check-point process states of each instance, the layout psg_run_batch_spec
+    traces on the device: flat int32 [count][R+1][9][n] (Option None = INT32_MIN).
+    init: optional [count][n] initial values (else seeded)."""
+    per = (cfg.rounds + 1) * NFIELDS * cfg.n
+    out = (C.c_int32 * (count * per))()
+    init_arr = None
+    if init is not None:
+        flat = [int(v) for row in init for v in row]
+        init_arr = (C.c_int32 * len(flat))(*flat)
+    _check(lib().oracle_trace(C.byref(cfg), inst_begin, count, init_arr, out, threads))
+    return out
+
+
+def vm_run(program, tr, count, n, rounds):
+    """Evaluate a compiled Spec (round_amd.formula.Program) on traces with the CPU
+    interpreter: returns ([first_fail per slot] per instance, [term_round])."""
+    cp = program.to_c()
+    ff = (C.c_uint8 * (count * abi.PSG_MAX_CHECKS))()
+    tm = (C.c_uint8 * count)()
+    _check(lib().oracle_vm_run(C.byref(cp), tr, count, n, rounds, ff, tm))
+    k = len(program.slot_entry)
+    return [list(ff[i * abi.PSG_MAX_CHECKS:i * abi.PSG_MAX_CHECKS + k]) for i in range(count)], list(tm)

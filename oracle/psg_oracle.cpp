@@ -1285,6 +1285,7 @@ struct InstOut {
   psg_instance_summary sum;
   std::vector<psg_process_record> rec;
   std::vector<double> fdec, fx; /* real-valued algorithms: Double decision / final x per process */
+  std::vector<int32_t>* vtrace = nullptr; /* Spec-program trace: [R+1][F][n] int32, None = INT32_MIN */
   std::vector<int64_t> trace; /* optional: per check point, per process F_X / decided */
   bool mismatch = false;
   std::string msg;
@@ -1376,6 +1377,10 @@ static void run_engine(Alg& alg, const psg_config& cfg, uint64_t inst, const int
     for (int i = 0; i < nck; ++i)
       if (!ck[i] && S.first_fail[i] == PSG_NEVER) S.first_fail[i] = (uint8_t)c;
     if (term && S.term_round == PSG_NEVER) S.term_round = (uint8_t)c;
+    if (out.vtrace)
+      for (int f = 0; f < F_NFIELDS; ++f)
+        for (int p = 0; p < n; ++p)
+          out.vtrace->push_back(fcur[f][p] == NONE ? INT32_MIN : (int32_t)fcur[f][p]);
     if (want_trace) {
       for (int p = 0; p < n; ++p) out.trace.push_back(fcur[F_X][p]);
       for (int p = 0; p < n; ++p) out.trace.push_back(fcur[F_DECIDED][p]);
@@ -1470,6 +1475,124 @@ static void run_one(const psg_config& cfg, uint64_t inst, const int32_t* init, i
     case PSG_ALG_KSET_ES: { KSetES a{cfg.n, cfg.param, cfg.param2, cfg.variant}; run_engine(a, cfg, inst, init, spec_mode, eho, out, trace); break; }
   }
 }
+
+/* ------------------------------------------------------------------ */
+/* Spec-program interpreter (CPU reference of psg_spec_vm.hip)          */
+/* ------------------------------------------------------------------ */
+/* Executes the bytecode of include/psg.h scalar-wise: lane-form process
+ * quantifiers are plain loops over pids (the lane form is only the device's
+ * evaluation strategy), V.exists over Int visits the same finitized candidate
+ * set (distinct values of the compared fields / expressions, +-1, MIN, MAX). */
+struct CpuVm {
+  const psg_spec_program& P;
+  const int32_t *cur, *old, *init;
+  int n, r;
+  int32_t var[16] = {0};
+  int err = 0;
+
+  int32_t field(int f, int tag, int32_t p) const {
+    if (p < 0 || p >= n || f < 0 || f >= F_NFIELDS) return 0;
+    const int32_t* t = tag == T_CUR ? cur : (tag == T_OLD ? old : init);
+    return t[f * n + p];
+  }
+  static int32_t binop(int op, int32_t x, int32_t y) {
+    switch (op) {
+      case PSG_OP_AND: return x != 0 && y != 0;
+      case PSG_OP_OR: return x != 0 || y != 0;
+      case PSG_OP_IMPL: return x == 0 || y != 0;
+      case PSG_OP_EQ: return x == y;
+      case PSG_OP_NE: return x != y;
+      case PSG_OP_LT: return x < y;
+      case PSG_OP_LE: return x <= y;
+      case PSG_OP_GT: return x > y;
+      case PSG_OP_GE: return x >= y;
+      case PSG_OP_ADD: return (int32_t)((uint32_t)x + (uint32_t)y);
+      case PSG_OP_SUB: return (int32_t)((uint32_t)x - (uint32_t)y);
+      case PSG_OP_MUL: return (int32_t)((uint32_t)x * (uint32_t)y);
+      case PSG_OP_DIV: return y == 0 ? 0 : (x == INT32_MIN && y == -1) ? x : x / y;
+      default: return (y == 0 || y == -1) ? 0 : x % y;
+    }
+  }
+  /* Run code from pc with the given stack until HALT (returns top) or until the
+   * QEND that closes the current quantifier body (returns the body value and the
+   * pc of that QEND through *endpc). */
+  int32_t run(int pc, std::vector<int32_t>& st, int* endpc) {
+    const int32_t* code = P.code;
+    while (pc < P.n_words) {
+      const int32_t w = code[pc];
+      const int op = w & 0xff, a = (w >> 8) & 0xff, b = w >> 16;
+      ++pc;
+      switch (op) {
+        case PSG_OP_HALT: return st.empty() ? 0 : st.back();
+        case PSG_OP_IMM: st.push_back(b); break;
+        case PSG_OP_IMM32: st.push_back(code[pc++]); break;
+        case PSG_OP_N: st.push_back(n); break;
+        case PSG_OP_R: st.push_back(r); break;
+        case PSG_OP_COORD: st.push_back((r / 4) % n); break;
+        case PSG_OP_VAR: st.push_back(var[a]); break;
+        case PSG_OP_FIELD: { int32_t p = st.back(); st.back() = field(a, b, p); break; }
+        case PSG_OP_NOT: st.back() = st.back() == 0; break;
+        case PSG_OP_NEG: st.back() = (int32_t)(0u - (uint32_t)st.back()); break;
+        case PSG_OP_ISDEF: st.back() = st.back() != INT32_MIN; break;
+        case PSG_OP_BIND: var[a] = st.back(); st.pop_back(); break;
+        case PSG_OP_QEND: if (endpc) *endpc = pc - 1; return st.empty() ? 0 : st.back();
+        case PSG_OP_QBEGIN: {
+          const int end = code[pc++];
+          std::vector<int64_t> cands;
+          if (a == PSG_Q_EXISTS_VI) {
+            const int32_t desc = code[pc++];
+            const int nexpr = desc & 0xffff, nfs = (desc >> 16) & 0xffff;
+            std::set<int32_t> bases;
+            for (int e = 0; e < nexpr; ++e) { bases.insert(st.back()); st.pop_back(); }
+            for (int f = 0; f < nfs; ++f) {
+              const int32_t fw = code[pc++];
+              for (int p = 0; p < n; ++p) bases.insert(field(fw & 0xff, (fw >> 8) & 0xff, p));
+            }
+            for (int32_t v : bases)
+              for (int d = -1; d <= 1; ++d) cands.push_back((int32_t)((uint32_t)v + (uint32_t)d));
+            cands.push_back(INT32_MIN);
+            cands.push_back(INT32_MAX);
+          } else if (a == PSG_Q_EXISTS_VB) {
+            cands = {0, 1};
+          } else {
+            for (int p = 0; p < n; ++p) cands.push_back(p);
+          }
+          const bool forall = a == PSG_Q_FORALL_P || a == PSG_Q_FORALL_PL;
+          const bool count = a == PSG_Q_COUNT_P || a == PSG_Q_COUNT_PL;
+          int32_t acc = forall ? 1 : 0;
+          for (int64_t cv : cands) {
+            var[b] = (int32_t)cv;
+            std::vector<int32_t> sub;
+            int e = -1;
+            const int32_t res = run(pc, sub, &e);
+            if (e != end) { err = 1; return 0; }
+            if (count) acc += res != 0;
+            else if (forall) { if (res == 0) { acc = 0; break; } }
+            else if (res != 0) { acc = 1; break; }
+          }
+          st.push_back(acc);
+          pc = end + 1;
+          break;
+        }
+        default: {
+          if (op >= PSG_OP_AND && op <= PSG_OP_MOD) {
+            int32_t y = st.back(); st.pop_back();
+            st.back() = binop(op, st.back(), y);
+          } else {
+            err = 1;
+            return 0;
+          }
+        }
+      }
+    }
+    err = 1;
+    return 0;
+  }
+  int32_t eval(int pc) {
+    std::vector<int32_t> st;
+    return run(pc, st, nullptr);
+  }
+};
 
 } // namespace orc
 
@@ -1589,6 +1712,57 @@ static int run_impl(const psg_config* cfg, uint64_t inst_begin, uint64_t count, 
   if (bad) {
     for (auto& e : errs) if (!e.empty()) { g_oracle_err = e; break; }
     return PSG_EIO;
+  }
+  return 0;
+}
+
+/* Spec-program trace of instances [inst_begin, inst_begin+count) (init: optional
+ * [count][n] initial values, else seeded): out receives
+ * count x (R+1) x F x n int32 (the device trace layout; Option None = INT32_MIN). */
+int oracle_trace(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const int32_t* init, int32_t* out,
+                 int32_t threads) {
+  std::string err;
+  int rc = orc::validate(cfg, err);
+  if (rc) { g_oracle_err = err; return rc; }
+  if (threads < 1) threads = 1;
+  const uint64_t per = (uint64_t)(cfg->rounds + 1) * orc::F_NFIELDS * (uint64_t)cfg->n;
+  auto worker = [&](int t) {
+    uint64_t lo = count * (uint64_t)t / threads, hi = count * (uint64_t)(t + 1) / threads;
+    for (uint64_t i = lo; i < hi; ++i) {
+      orc::InstOut o;
+      std::vector<int32_t> tr;
+      o.vtrace = &tr;
+      orc::run_one(*cfg, inst_begin + i, init ? init + i * (uint64_t)cfg->n : nullptr, 0, nullptr, o, false);
+      std::memcpy(out + i * per, tr.data(), sizeof(int32_t) * per);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t) th.emplace_back(worker, t);
+  worker(0);
+  for (auto& x : th) x.join();
+  return 0;
+}
+
+/* Evaluate a Spec program over traces (count x (R+1) x F x n): first_fail
+ * [count][PSG_MAX_CHECKS] and term_round [count] in psg_instance_summary terms. */
+int oracle_vm_run(const psg_spec_program* prog, const int32_t* trace, uint64_t count, int32_t n, int32_t R,
+                  uint8_t* first_fail, uint8_t* term_round) {
+  const uint64_t row = (uint64_t)orc::F_NFIELDS * (uint64_t)n;
+  for (uint64_t i = 0; i < count; ++i) {
+    const int32_t* base = trace + i * (uint64_t)(R + 1) * row;
+    uint8_t* ff = first_fail + i * PSG_MAX_CHECKS;
+    for (int s = 0; s < PSG_MAX_CHECKS; ++s) ff[s] = PSG_NEVER;
+    term_round[i] = PSG_NEVER;
+    for (int c = 0; c <= R; ++c) {
+      orc::CpuVm vm{*prog, base + (uint64_t)c * row, base + (uint64_t)(c > 0 ? c - 1 : 0) * row, base, n, c};
+      for (int s = 0; s < prog->n_slots; ++s) {
+        const bool vac = c == 0 && (prog->slot_flags[s] & PSG_SPEC_RELATIONAL);
+        if (!vac && vm.eval(prog->slot_entry[s]) == 0 && ff[s] == PSG_NEVER) ff[s] = (uint8_t)c;
+      }
+      if (prog->term_entry >= 0 && term_round[i] == PSG_NEVER && vm.eval(prog->term_entry) != 0)
+        term_round[i] = (uint8_t)c;
+      if (vm.err) { g_oracle_err = "bad spec program"; return PSG_EINVAL; }
+    }
   }
   return 0;
 }

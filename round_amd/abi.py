@@ -186,3 +186,16 @@ def summary_dict(s, alg, rounds):
         "term_hist": [s.term_hist[i] for i in range(rounds + 2)],
         "kernel_ns": s.kernel_ns,
     }
+
+
+class SpecProgram(C.Structure):
+    """psg_spec_program (include/psg.h): a compiled Spec (round_amd/formula.py)."""
+    _fields_ = [
+        ("n_slots", C.c_int32),
+        ("n_words", C.c_int32),
+        ("code", C.POINTER(C.c_int32)),
+        ("slot_entry", C.POINTER(C.c_int32)),
+        ("slot_flags", C.POINTER(C.c_int32)),
+        ("term_entry", C.c_int32),
+        ("n_vars", C.c_int32),
+    ]

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -54,6 +55,12 @@ struct psg_ctx {
   bool init_f64_host = false;    // false: seeded Doubles generated inside the round kernel
   double* d_dec_f64 = nullptr;
   double* d_rec_f64 = nullptr;   // fetch path: [k][n][2] (decision, final x)
+  int32_t* d_trace = nullptr;    // psg_run_batch_spec: state trace of one chunk
+  uint64_t trace_cap = 0;        // instances the trace buffer holds
+  unsigned long long* d_vm_counters = nullptr;
+  int32_t* d_vm_err = nullptr;
+  int32_t* d_prog = nullptr;     // code | slot_entry | slot_flags
+  size_t prog_cap = 0;
   bool staged = false;
   uint64_t staged_begin = 0, staged_count = 0;
   int32_t* d_dec = nullptr;
@@ -477,6 +484,46 @@ int psg_run_batch(psg_ctx* c, uint64_t inst_begin, uint64_t count, psg_summary* 
   return PSG_OK;
 }
 
+static int validate_prog(const psg_spec_program* p, std::string& m) {
+  if (!p || !p->code || !p->slot_entry || !p->slot_flags) { m = "null spec program"; return PSG_EINVAL; }
+  if (p->n_slots < 1 || p->n_slots > PSG_MAX_CHECKS) { m = "spec program needs 1..12 slots"; return PSG_EINVAL; }
+  if (p->n_words < 1 || p->n_words > (1 << 20)) { m = "bad spec program length"; return PSG_EINVAL; }
+  if (p->n_vars < 0 || p->n_vars > 16) { m = "spec program uses more than 16 bound variables"; return PSG_EINVAL; }
+  for (int s = 0; s < p->n_slots; ++s)
+    if (p->slot_entry[s] < 0 || p->slot_entry[s] >= p->n_words) { m = "slot entry out of range"; return PSG_EINVAL; }
+  if (p->term_entry >= p->n_words) { m = "termination entry out of range"; return PSG_EINVAL; }
+  // structural check: opcodes known, quantifier ends in range, variables in range
+  for (int pc = 0; pc < p->n_words;) {
+    const int32_t w = p->code[pc];
+    const int op = w & 0xff, a = (w >> 8) & 0xff;
+    if (op > PSG_OP_COORD) { m = "unknown opcode at " + std::to_string(pc); return PSG_EINVAL; }
+    if ((op == PSG_OP_VAR || op == PSG_OP_BIND) && a >= 16) { m = "variable out of range"; return PSG_EINVAL; }
+    if (op == PSG_OP_FIELD && (a >= PSG_NFIELDS || (w >> 16) < 0 || (w >> 16) > PSG_TAG_INIT)) {
+      m = "bad field / tag at " + std::to_string(pc);
+      return PSG_EINVAL;
+    }
+    ++pc;
+    if (op == PSG_OP_IMM32) ++pc;
+    if (op == PSG_OP_QBEGIN) {
+      if (a > PSG_Q_EXISTS_VI || (w >> 16) < 0 || (w >> 16) >= 16 || pc >= p->n_words) {
+        m = "bad quantifier at " + std::to_string(pc - 1);
+        return PSG_EINVAL;
+      }
+      const int32_t end = p->code[pc];
+      if (end <= pc || end >= p->n_words || (p->code[end] & 0xff) != PSG_OP_QEND) {
+        m = "quantifier end mismatch at " + std::to_string(pc - 1);
+        return PSG_EINVAL;
+      }
+      ++pc;
+      if (a == PSG_Q_EXISTS_VI) {
+        if (pc >= p->n_words) { m = "truncated V.exists"; return PSG_EINVAL; }
+        pc += 1 + ((p->code[pc] >> 16) & 0xffff);
+      }
+    }
+  }
+  return PSG_OK;
+}
+
 int psg_copy_decisions(psg_ctx* c, int32_t* decision, int32_t* decision_round) {
   if (!c) return PSG_EINVAL;
   HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -490,6 +537,113 @@ int psg_copy_decisions(psg_ctx* c, int32_t* decision, int32_t* decision_round) {
     for (uint64_t k = 0; k < cells; ++k) decision_round[k] = tmp[k] == 0xFF ? -1 : (int32_t)tmp[k];
     delete[] tmp;
   }
+  return PSG_OK;
+}
+
+int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const psg_spec_program* prog,
+                       psg_summary* out, psg_instance_summary* per_inst) {
+  if (!c) return PSG_EINVAL;
+  if (c->cfg.alg == PSG_ALG_EPSILON) return fail(c, PSG_EINVAL, "Spec programs need integer state (not EpsilonConsensus)");
+  std::string m;
+  if (validate_prog(prog, m)) return fail(c, PSG_EINVAL, m);
+  if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  if (out) std::memset(out, 0, sizeof(*out));
+  if (count == 0) return PSG_OK;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const int n = c->cfg.n, R = c->cfg.rounds;
+  // program: code | slot_entry | slot_flags
+  const size_t words = (size_t)prog->n_words + 2 * (size_t)prog->n_slots;
+  if (words > c->prog_cap) {
+    if (c->d_prog) (void)hipFree(c->d_prog);
+    c->d_prog = nullptr;
+    c->prog_cap = 0;
+    HIPCHK(c, hipMalloc(&c->d_prog, sizeof(int32_t) * words));
+    c->prog_cap = words;
+  }
+  HIPCHK(c, hipMemcpy(c->d_prog, prog->code, sizeof(int32_t) * prog->n_words, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_prog + prog->n_words, prog->slot_entry, sizeof(int32_t) * prog->n_slots,
+                      hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_prog + prog->n_words + prog->n_slots, prog->slot_flags, sizeof(int32_t) * prog->n_slots,
+                      hipMemcpyHostToDevice));
+  // trace chunk: <= PSG_SPEC_TRACE_MB (default 2048) MiB of [R+1][fields][n] int32 rows
+  uint64_t budget = 2048ull << 20;
+  if (const char* e = std::getenv("PSG_SPEC_TRACE_MB")) {
+    const long long mb = std::atoll(e);
+    if (mb > 0) budget = (uint64_t)mb << 20;
+  }
+  const uint64_t per_inst_bytes = (uint64_t)(R + 1) * PSG_NFIELDS * (uint64_t)n * sizeof(int32_t);
+  const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(count, budget / per_inst_bytes));
+  if (chunk > c->trace_cap) {
+    if (c->d_trace) (void)hipFree(c->d_trace);
+    c->d_trace = nullptr;
+    c->trace_cap = 0;
+    HIPCHK(c, hipMalloc(&c->d_trace, per_inst_bytes * chunk));
+    c->trace_cap = chunk;
+  }
+  if (!c->d_vm_counters) HIPCHK(c, hipMalloc(&c->d_vm_counters, sizeof(unsigned long long) * NCOUNTERS));
+  if (!c->d_vm_err) HIPCHK(c, hipMalloc(&c->d_vm_err, sizeof(int32_t)));
+  HIPCHK(c, hipMemsetAsync(c->d_vm_err, 0, sizeof(int32_t), c->stream));
+  const bool staged = c->staged && c->staged_begin == inst_begin && c->staged_count == count;
+  psg_summary acc;
+  std::memset(&acc, 0, sizeof(acc));
+  int vm_grid = 0;
+  HIPCHK(c, hipDeviceGetAttribute(&vm_grid, hipDeviceAttributeMultiprocessorCount, c->cfg.device));
+  vm_grid *= 8;
+  for (uint64_t off = 0; off < count; off += chunk) {
+    const uint64_t m_cnt = std::min<uint64_t>(chunk, count - off);
+    KArgs a = make_args(c);
+    a.inst_begin = inst_begin + off;
+    a.count = m_cnt;
+    a.init = staged ? c->d_init + off * (uint64_t)n : nullptr;  // else seeded by the kernel
+    a.out_decision = c->d_dec + off * (uint64_t)n;
+    a.out_dround = c->d_dround + off * (uint64_t)n;
+    a.out_inst = c->d_inst + off;
+    a.trace = c->d_trace;
+    psg_summary part;
+    int rc = run_kernel(c, a, m_cnt, &part, true);
+    if (rc) return rc;
+    VmArgs v;
+    v.code = c->d_prog;
+    v.slot_entry = c->d_prog + prog->n_words;
+    v.slot_flags = c->d_prog + prog->n_words + prog->n_slots;
+    v.n_slots = prog->n_slots;
+    v.term_entry = prog->term_entry;
+    v.n_words = prog->n_words;
+    v.trace = c->d_trace;
+    v.count = m_cnt;
+    v.n = n;
+    v.R = R;
+    v.out_inst = c->d_inst + off;
+    v.counters = c->d_vm_counters;
+    v.err = c->d_vm_err;
+    HIPCHK(c, hipMemsetAsync(c->d_vm_counters, 0, sizeof(unsigned long long) * NCOUNTERS, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_spec_vm(v, (int)std::min<uint64_t>(m_cnt, (uint64_t)vm_grid), c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    unsigned long long host[NCOUNTERS];
+    HIPCHK(c, hipMemcpyAsync(host, c->d_vm_counters, sizeof(host), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    acc.instances += part.instances;
+    acc.process_rounds += part.process_rounds;
+    acc.decided_processes += part.decided_processes;
+    acc.digest = (int64_t)((uint64_t)acc.digest + (uint64_t)part.digest);
+    acc.kernel_ns += part.kernel_ns + (int64_t)((double)ms * 1e6);
+    for (int i = 0; i < PSG_MAX_CHECKS; ++i) acc.fail_count[i] += (int64_t)host[C_FAIL + i];
+    for (int i = 0; i < R + 2; ++i) acc.term_hist[i] += (int64_t)host[C_HIST + i];
+  }
+  int32_t verr = 0;
+  HIPCHK(c, hipMemcpy(&verr, c->d_vm_err, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (verr) {
+    return fail(c, PSG_ERANGE,
+                std::string("spec program exceeded interpreter limits (flags ") + std::to_string(verr) +
+                    "; 1 stack > 24, 2 nesting > 12, 4 V.exists candidates > 1024 or nesting > 2, 8 bad opcode)");
+  }
+  c->last_count = count;
+  if (per_inst)
+    HIPCHK(c, hipMemcpy(per_inst, c->d_inst, sizeof(psg_instance_summary) * count, hipMemcpyDeviceToHost));
+  if (out) *out = acc;
   return PSG_OK;
 }
 
@@ -582,6 +736,10 @@ void psg_destroy(psg_ctx* c) {
   if (c->d_init_f64) (void)hipFree(c->d_init_f64);
   if (c->d_dec_f64) (void)hipFree(c->d_dec_f64);
   if (c->d_rec_f64) (void)hipFree(c->d_rec_f64);
+  if (c->d_trace) (void)hipFree(c->d_trace);
+  if (c->d_vm_counters) (void)hipFree(c->d_vm_counters);
+  if (c->d_vm_err) (void)hipFree(c->d_vm_err);
+  if (c->d_prog) (void)hipFree(c->d_prog);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);

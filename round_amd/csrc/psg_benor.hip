@@ -68,10 +68,17 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
     Checks ck;
     ck.reset();
     benor_check<W>(g, ck, 0, false, n, full, x, cd, vote, decided, decision, false, false, true);
+    // vote: Option[Boolean] (PSG_NONE32 when empty)
+    auto trace = [&](int c, int32_t hs) {
+      trace_put<W>(g, a, i, c, x ? 1 : 0, decided ? 1 : 0, decision ? 1 : 0, 0, 0, 0, vote < 0 ? PSG_NONE32 : vote,
+                   cd ? 1 : 0, hs);
+    };
+    if (a.trace) trace(0, n);
     for (int k = 0; k < a.R; ++k) {
       const bool old_decided = decided, old_decision = decision;
       const Mask<W> act = g.ballot(!halted);
       bool pred = true;
+      int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
@@ -82,6 +89,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
         }
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const int size = mpopc(M);
+        if (!halted) hs = size;
         pred = !g.any(!halted && size <= n / 2);
         if ((k & 1) == 0) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
           const Mask<W> Tm = mand(g.ballot(x), act);
@@ -129,6 +137,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
         if (halt_round == k) halted = true;
       }
       benor_check<W>(g, ck, k + 1, true, n, full, x, cd, vote, decided, decision, old_decided, old_decision, pred);
+      if (a.trace) trace(k + 1, hs);
     }
     finish_instance<W>(g, a, i, ck, 5, dec_val, dec_round, halt_round, x ? 1 : 0, &bc);
   }

@@ -33,10 +33,25 @@ struct KArgs {
   double* out_dec_f64;               // nullable: [count][n] Double decisions
   double* out_rec_f64;               // nullable: [count][n][2] (decision, final x) for the fetch path
   double real_param;                 // EpsilonConsensus epsilon
+  int32_t* trace;                    // nullable: Spec-program trace [count][R+1][PSG_NFIELDS][n]
   int32_t n, R, V, param, param2, variant, tiebreak;
   uint32_t drop_log2, good_p32;
   int32_t good_min, crash_fmax, ho_min;
   uint32_t self_bit;
+};
+
+// Spec-program interpreter arguments (psg_spec_vm.hip)
+struct VmArgs {
+  const int32_t* code;
+  const int32_t* slot_entry;
+  const int32_t* slot_flags;
+  int32_t n_slots, term_entry, n_words;
+  const int32_t* trace;  // [count][R+1][PSG_NFIELDS][n]
+  uint64_t count;
+  int32_t n, R;
+  psg_instance_summary* out_inst;
+  unsigned long long* counters;  // NCOUNTERS (fail counts, termination histogram)
+  int32_t* err;                  // OR of VM_ERR_* over all instances
 };
 
 // global counter layout (uint64 each)
@@ -712,6 +727,26 @@ PSG_DEV void finish_instance(Grp<W>& g, const KArgs& a, uint64_t i, const Checks
       atomicAdd(&bc->digest, (unsigned long long)dig);
     }
   }
+}
+
+// Process state at check point c for the Spec-program interpreter
+// (psg_run_batch_spec): trace[i][c][field][pid], one coalesced row per field.
+template <int W>
+PSG_DEV void trace_put(const Grp<W>& g, const KArgs& a, uint64_t i, int c, int32_t x, int32_t decided,
+                       int32_t decision, int32_t ts, int32_t ready, int32_t commit, int32_t vote, int32_t cand,
+                       int32_t hosize) {
+  if (!g.valid) return;
+  const uint64_t n = (uint64_t)a.n;
+  int32_t* t = a.trace + (i * (uint64_t)(a.R + 1) + (uint64_t)c) * PSG_NFIELDS * n + (uint64_t)g.pid;
+  t[PSG_FIELD_X * n] = x;
+  t[PSG_FIELD_DECIDED * n] = decided;
+  t[PSG_FIELD_DECISION * n] = decision;
+  t[PSG_FIELD_TS * n] = ts;
+  t[PSG_FIELD_READY * n] = ready;
+  t[PSG_FIELD_COMMIT * n] = commit;
+  t[PSG_FIELD_VOTE * n] = vote;
+  t[PSG_FIELD_CANDECIDE * n] = cand;
+  t[PSG_FIELD_HOSIZE * n] = hosize;
 }
 
 // Group geometry: W == 1 -> 4 independent instances per 256-thread block;

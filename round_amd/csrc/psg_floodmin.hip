@@ -57,8 +57,13 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
       kagree_check<W>(g, ck, c, 1, full, decided, decision, X0, crashed, L.ds);
     };
     check(0);
+    auto trace = [&](int c, int32_t hs) {
+      trace_put<W>(g, a, i, c, x, decided ? 1 : 0, decision, 0, 0, 0, 0, 0, hs);
+    };
+    if (a.trace) trace(0, n);
     for (int k = 0; k < a.R; ++k) {
       const Mask<W> act = g.ballot(!halted);
+      int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
@@ -68,6 +73,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
           CN = g.ballot(sc.crash_round == k);
         }
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+        if (a.trace && !halted) hs = mpopc(M);
         // x = min(x, min{x_q : q in M}) by ascending distinct sender values
         bool unres = !halted;
         int32_t nx = x;
@@ -99,6 +105,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
         }
       }
       check(k + 1);
+      if (a.trace) trace(k + 1, hs);
     }
     finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, x, &bc);
   }

@@ -90,8 +90,13 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
       kagree_check<W>(g, ck, c, kk, full, decided, decision, X0, crashed, ds);
     };
     check(0);
+    auto trace = [&](int c, int32_t hs) {
+      trace_put<W>(g, a, i, c, kset_pick<W>(t, x0s), decided ? 1 : 0, decision, 0, 0, 0, 0, 0, hs);
+    };
+    if (a.trace) trace(0, n);
     for (int k = 0; k < a.R; ++k) {
       const Mask<W> act = g.ballot(!halted);
+      int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
@@ -101,6 +106,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
           CN = g.ballot(sc.crash_round == k);
         }
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+        if (a.trace && !halted) hs = mpopc(M);
         const Mask<W> Dm = mand(g.ballot(decider), act);  // senders' decider flags (pre-state)
 #pragma unroll
         for (int w = 0; w < W; ++w) ts[g.pid * W + w] = t.w[w];
@@ -195,6 +201,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
         if (halt_round == k) halted = true;
       }
       check(k + 1);
+      if (a.trace) trace(k + 1, hs);
     }
     const int32_t mainx = g.valid ? kset_pick<W>(t, x0s) : 0;
     finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, mainx, &bc);

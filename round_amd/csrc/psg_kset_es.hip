@@ -60,8 +60,13 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_es_kernel(KArgs a)
       kagree_check<W>(g, ck, c, kk, full, decided, decision, X0, crashed, L.ds);
     };
     check(0);
+    auto trace = [&](int c, int32_t hs) {
+      trace_put<W>(g, a, i, c, est, decided ? 1 : 0, decision, 0, 0, 0, 0, 0, hs);
+    };
+    if (a.trace) trace(0, n);
     for (int k = 0; k < a.R; ++k) {
       const Mask<W> act = g.ballot(!halted);
+      int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
@@ -72,6 +77,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_es_kernel(KArgs a)
         }
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const int currNb = mpopc(M);
+        if (!halted) hs = currNb;
         const bool anyCD = many(mand(M, g.ballot(cd)));  // mailbox.exists(_._2._2), pre-update flags
         const bool decideNow = !halted && (k > t / kk || cd);
         // est = min over the mailbox's estimates (unchanged if the mailbox is empty)
@@ -106,6 +112,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_es_kernel(KArgs a)
         }
       }
       check(k + 1);
+      if (a.trace) trace(k + 1, hs);
     }
     finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, est, &bc);
   }

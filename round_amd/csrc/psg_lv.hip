@@ -148,11 +148,17 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
     Checks ck;
     ck.reset();
     lv_check<W>(g, L, X0, ck, 0, false, n, full, x, ts, vote, decision, fl, 0u, -1);
+    auto trace = [&](int c, int32_t hs) {
+      trace_put<W>(g, a, i, c, x, (fl & F_DECIDED) ? 1 : 0, decision, ts, (fl & F_READY) ? 1 : 0,
+                   (fl & F_COMMIT) ? 1 : 0, vote, 0, hs);
+    };
+    if (a.trace) trace(0, n);
 
     for (int k = 0; k < a.R; ++k) {
       const uint32_t old_fl = fl;
       const int32_t old_decision = decision;
       const Mask<W> act = g.ballot((fl & F_HALTED) == 0u);
+      int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
         const int32_t phase = k >> 2;
         const int c = phase % n;
@@ -171,6 +177,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
           case 0: {  // R0: send (x, ts) to coord; coord picks vote = x of maxBy ts
             const Mask<W> Mc = mand(ho_of<W>(g, L, HO, c), act);
             const int size = mpopc(Mc);
+            hs = g.pid == c ? size : 0;
             if (cAlive && (size > n / 2 || (k == 0 && size > 0))) {
               const int32_t v = maxby_ts_x<W>(g, L.xs, Mc, size, x, ts, myh, a.tiebreak);
               if (g.pid == c) {
@@ -182,6 +189,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
           }
           case 1: {  // R1: coord broadcasts vote if commit; receivers adopt (x, ts = r/4)
             const bool sent = cAlive && mtest(g.ballot((fl & F_COMMIT) != 0u), c);
+            hs = sent && mtest(HO, c) ? 1 : 0;
             if (sent) {
               const int32_t vc = g.bcast(vote, L.votes, c);
               const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
@@ -192,11 +200,13 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
           }
           case 2: {  // R2: ts == r/4 send x to coord; coord ready on a majority
             const Mask<W> Mc = mand(mand(ho_of<W>(g, L, HO, c), act), g.ballot(ts == phase));
+            hs = g.pid == c ? mpopc(Mc) : 0;
             if (cAlive && mpopc(Mc) > need2 && g.pid == c) fl |= F_READY;
             break;
           }
           default: {  // R3: coord broadcasts vote if ready; receivers decide and exit
             const bool sent = cAlive && mtest(g.ballot((fl & F_READY) != 0u), c);
+            hs = sent && mtest(HO, c) ? 1 : 0;
             if (sent) {
               const int32_t vc = g.bcast(vote, L.votes, c);
               const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
@@ -214,6 +224,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
         }
       }
       lv_check<W>(g, L, X0, ck, k + 1, true, n, full, x, ts, vote, decision, fl, old_fl, old_decision);
+      if (a.trace) trace(k + 1, (old_fl & F_HALTED) ? n : hs);
     }
     finish_instance<W>(g, a, i, ck, 7, dec_val, dec_round, halt_round, x, &bc);
   }

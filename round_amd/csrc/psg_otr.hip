@@ -100,11 +100,17 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
     Checks ck;
     ck.reset();
     otr_check<W, V2>(g, L, X0, ck, 0, false, n, full, x, dec01, decision, 0u, -1, valid01);
+    // OTR2's decision is an Option (PSG_NONE32 when empty)
+    auto trace = [&](int c, int32_t hs) {
+      trace_put<W>(g, a, i, c, x, (int32_t)dec01, V2 && !dec01 ? PSG_NONE32 : decision, 0, 0, 0, 0, 0, hs);
+    };
+    if (a.trace) trace(0, n);
 
     for (int k = 0; k < a.R; ++k) {
       const uint32_t old01 = dec01;
       const int32_t old_decision = decision;
       const Mask<W> act = g.ballot(halted01 == 0u);
+      int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
@@ -115,7 +121,9 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
         }
         // mailbox: broadcast(x) from every alive sender in HO(p)
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
-        const uint32_t upd = (1u - halted01) & gt01(mpopc(M), thr);
+        const int32_t msize = mpopc(M);
+        if (a.trace) hs = halted01 ? n : msize;
+        const uint32_t upd = (1u - halted01) & gt01(msize, thr);
         if (g.any(upd != 0u)) {
           if constexpr (W > 1) {
             L.xs[g.pid] = x;
@@ -151,6 +159,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
         halted01 |= h;
       }
       otr_check<W, V2>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, old01, old_decision, valid01);
+      if (a.trace) trace(k + 1, hs);
     }
     finish_instance<W>(g, a, i, ck, 8, dec_val, dec_round, halt_round, x, &bc);
   }

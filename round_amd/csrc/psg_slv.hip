@@ -94,9 +94,15 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
       kagree_check<W>(g, ck, c, 1, full, (fl & S_DECIDED) != 0u, decision, X0, false, L.ds);
     };
     check(0);
+    auto trace = [&](int c, int32_t hs) {
+      trace_put<W>(g, a, i, c, x, (fl & S_DECIDED) ? 1 : 0, decision, ts, 0, (fl & S_COMMIT) ? 1 : 0, vote, 0, hs);
+    };
+    if (a.trace) trace(0, n);
 
     for (int k = 0; k < a.R; ++k) {
       const Mask<W> act = g.ballot((fl & S_HALTED) == 0u);
+      const uint32_t fl_start = fl;
+      int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
         const int32_t r4 = k >> 2;
         const int c = r4 % n;
@@ -119,6 +125,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
         if (m3 == 0) {  // R0 (ShortLastVoting.scala:34-47)
           const Mask<W> Mc = mand(slv_ho_of<W>(g, L, HO, c), act);
           const int size = mpopc(Mc);
+          hs = g.pid == c ? size : 0;
           if (cAlive && size > n / 2) {
             const int32_t v = maxby_ts_x<W>(g, L.xs, Mc, size, x, ts, myh, a.tiebreak);
             if (g.pid == c) {
@@ -128,6 +135,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
           }
         } else if (m3 == 1) {  // R1 (ShortLastVoting.scala:51-69)
           const bool sent = cAlive && mtest(g.ballot((fl & S_COMMIT) != 0u), c);
+          hs = sent && mtest(HO, c) ? 1 : 0;
           if (sent) {
             const int32_t vc = g.bcast(vote, L.votes, c);
             const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
@@ -137,6 +145,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
         } else {  // R2 (ShortLastVoting.scala:72-98)
           const Mask<W> S = mand(act, g.ballot(ts == r4));
           const Mask<W> M = mand(HO, S);
+          hs = mpopc(M);
           const bool upd = live && mpopc(M) > need2 && (fl & S_DECIDED) == 0u;
           if (g.any(upd)) {
             const int32_t xs0 = g.bcast(x, L.xs, mfirst(S));
@@ -163,6 +172,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
         }
       }
       check(k + 1);
+      if (a.trace) trace(k + 1, (fl_start & S_HALTED) ? n : hs);
     }
     finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, x, &bc);
   }

@@ -1,0 +1,660 @@
+"""Spec formulas for the GPU checker: a Python mirror of the reference's Spec DSL
+and its compiler to the device bytecode (include/psg.h, psg_run_batch_spec).
+
+The reference writes a Spec as Scala expressions over the process state that the
+`Formula` macros (psync/macros/FormulaExtractor.scala:219-520) turn into a
+`Formula` tree (psync/formula/Formula.scala: ForAll / Exists / Comprehension /
+Cardinality, `init(...)` / `old(...)`, Option `isDefined` / `get`). The same
+specs read almost verbatim here, e.g. OTR's first invariant
+(example/Otr.scala:99-105):
+
+    ( P.forall(lambda i: ~i.decided)
+      | V.exists(lambda v: (P.filter(lambda i: i.x == v).size > 2 * n // 3)
+                           & P.forall(lambda i: i.decided.implies(i.decision == v))) )
+    & P.forall(lambda i: P.exists(lambda j1: i.x == init(j1.x)))
+
+Python operators: `&` `|` `~` for && || !, `.implies(b)` for ==>, `//` and `%`
+for Int division / remainder, comparisons as usual. `compile_spec` assembles the
+check slots exactly as the built-in checker does (psync/verification/
+Verifier.scala:111-141): slot "Safety" = some invariant holds, invariant i at
+check point r is `invariants(i) && (r % L != 0 ==> roundInvariants(r%L - 1)(0))`,
+then the properties ("Termination" becomes the termination round), then
+"SafetyPredicate" if the spec has one.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import itertools
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+from . import abi
+
+# --------------------------------------------------------------------------- ABI constants (include/psg.h)
+FIELD_X, FIELD_DECIDED, FIELD_DECISION, FIELD_TS, FIELD_READY, FIELD_COMMIT, FIELD_VOTE, FIELD_CANDECIDE, \
+    FIELD_HOSIZE = range(9)
+TAG_CUR, TAG_OLD, TAG_INIT = range(3)
+NONE32 = -(1 << 31)
+
+OP = dict(HALT=0, IMM=1, IMM32=2, N=3, R=4, VAR=5, FIELD=6, NOT=7, NEG=8, ISDEF=9, AND=10, OR=11, IMPL=12,
+          EQ=13, NE=14, LT=15, LE=16, GT=17, GE=18, ADD=19, SUB=20, MUL=21, DIV=22, MOD=23, BIND=24,
+          QBEGIN=25, QEND=26, COORD=27)
+Q_FORALL_P, Q_EXISTS_P, Q_COUNT_P, Q_FORALL_PL, Q_EXISTS_PL, Q_COUNT_PL, Q_EXISTS_VB, Q_EXISTS_VI = range(8)
+SPEC_RELATIONAL = 1
+MAX_VARS = 16
+
+# fields each algorithm's kernels trace (the rest read as 0)
+ALG_FIELDS = {
+    abi.PSG_ALG_OTR: {FIELD_X, FIELD_DECIDED, FIELD_DECISION, FIELD_HOSIZE},
+    abi.PSG_ALG_OTR2: {FIELD_X, FIELD_DECIDED, FIELD_DECISION, FIELD_HOSIZE},
+    abi.PSG_ALG_LAST_VOTING: {FIELD_X, FIELD_DECIDED, FIELD_DECISION, FIELD_TS, FIELD_READY, FIELD_COMMIT,
+                              FIELD_VOTE, FIELD_HOSIZE},
+    abi.PSG_ALG_FLOODMIN: {FIELD_X, FIELD_DECIDED, FIELD_DECISION, FIELD_HOSIZE},
+    abi.PSG_ALG_KSET: {FIELD_X, FIELD_DECIDED, FIELD_DECISION, FIELD_HOSIZE},
+    abi.PSG_ALG_BENOR: {FIELD_X, FIELD_DECIDED, FIELD_DECISION, FIELD_CANDECIDE, FIELD_VOTE, FIELD_HOSIZE},
+    abi.PSG_ALG_SLV: {FIELD_X, FIELD_DECIDED, FIELD_DECISION, FIELD_TS, FIELD_COMMIT, FIELD_VOTE, FIELD_HOSIZE},
+    abi.PSG_ALG_KSET_ES: {FIELD_X, FIELD_DECIDED, FIELD_DECISION, FIELD_HOSIZE},
+}
+
+
+class FormulaError(ValueError):
+    pass
+
+
+# --------------------------------------------------------------------------- expression tree
+class Expr:
+    """A Formula node. Operators build new nodes (they never evaluate)."""
+
+    def _bin(self, op, other, swap=False):
+        other = lift(other)
+        return Bin(op, other, self) if swap else Bin(op, self, other)
+
+    def __and__(self, o): return self._bin("AND", o)
+    def __rand__(self, o): return self._bin("AND", o, True)
+    def __or__(self, o): return self._bin("OR", o)
+    def __ror__(self, o): return self._bin("OR", o, True)
+    def __invert__(self): return Un("NOT", self)
+    def __neg__(self): return Un("NEG", self)
+    def __eq__(self, o): return self._bin("EQ", o)  # noqa: PLE0307 (builds a node)
+    def __ne__(self, o): return self._bin("NE", o)
+    def __lt__(self, o): return self._bin("LT", o)
+    def __le__(self, o): return self._bin("LE", o)
+    def __gt__(self, o): return self._bin("GT", o)
+    def __ge__(self, o): return self._bin("GE", o)
+    def __add__(self, o): return self._bin("ADD", o)
+    def __radd__(self, o): return self._bin("ADD", o, True)
+    def __sub__(self, o): return self._bin("SUB", o)
+    def __rsub__(self, o): return self._bin("SUB", o, True)
+    def __mul__(self, o): return self._bin("MUL", o)
+    def __rmul__(self, o): return self._bin("MUL", o, True)
+    def __floordiv__(self, o): return self._bin("DIV", o)  # Scala Int `/` (truncates)
+    def __rfloordiv__(self, o): return self._bin("DIV", o, True)
+    def __mod__(self, o): return self._bin("MOD", o)
+    def __rmod__(self, o): return self._bin("MOD", o, True)
+    __hash__ = object.__hash__
+
+    def implies(self, o):
+        """`a ==> b`."""
+        return self._bin("IMPL", o)
+
+    def __bool__(self):
+        raise FormulaError("a Formula has no truth value in Python: use & | ~ and .implies(), not and/or/not")
+
+    # Option[_] accessors (FormulaExtractor: isDefined / isEmpty / get)
+    @property
+    def isDefined(self): return Un("ISDEF", self)
+    @property
+    def isEmpty(self): return Un("NOT", Un("ISDEF", self))
+    @property
+    def get(self): return self
+
+    def children(self):
+        return ()
+
+
+class Lit(Expr):
+    def __init__(self, v):
+        if isinstance(v, bool):
+            v = int(v)
+        if not (-(1 << 31) <= int(v) < (1 << 31)):
+            raise FormulaError(f"literal {v} is not an Int")
+        self.v = int(v)
+
+
+class NVal(Expr):
+    pass
+
+
+class RVal(Expr):
+    pass
+
+
+class Var(Expr):
+    """A bound variable (process id, or a V.exists value)."""
+    _ids = itertools.count()
+
+    def __init__(self, kind):
+        self.kind = kind  # "proc" | "int" | "bool"
+        self.uid = next(Var._ids)
+
+    # process fields (the variables of the reference's Process classes)
+    @property
+    def x(self): return Field(FIELD_X, self)
+    @property
+    def decided(self): return Field(FIELD_DECIDED, self)
+    @property
+    def decision(self): return Field(FIELD_DECISION, self)
+    @property
+    def ts(self): return Field(FIELD_TS, self)
+    @property
+    def ready(self): return Field(FIELD_READY, self)
+    @property
+    def commit(self): return Field(FIELD_COMMIT, self)
+    @property
+    def vote(self): return Field(FIELD_VOTE, self)
+    @property
+    def canDecide(self): return Field(FIELD_CANDECIDE, self)
+    @property
+    def est(self): return Field(FIELD_X, self)
+    @property
+    def HO(self): return _HO(self)
+
+
+class _HO:
+    def __init__(self, p): self.p = p
+    @property
+    def size(self): return Field(FIELD_HOSIZE, self.p)
+
+
+class CoordVal(Expr):
+    """coord = (r/4) % n as a process (LastVoting.scala:95)."""
+    @property
+    def commit(self): return Field(FIELD_COMMIT, self)
+    @property
+    def ready(self): return Field(FIELD_READY, self)
+    @property
+    def vote(self): return Field(FIELD_VOTE, self)
+    @property
+    def x(self): return Field(FIELD_X, self)
+    @property
+    def ts(self): return Field(FIELD_TS, self)
+
+
+class Field(Expr):
+    def __init__(self, f, proc, tag=TAG_CUR):
+        self.f, self.proc, self.tag = f, lift(proc), tag
+
+    def children(self):
+        return (self.proc,)
+
+
+class Un(Expr):
+    def __init__(self, op, x):
+        self.op, self.x = op, lift(x)
+
+    def children(self):
+        return (self.x,)
+
+
+class Bin(Expr):
+    def __init__(self, op, x, y):
+        self.op, self.x, self.y = op, lift(x), lift(y)
+
+    def children(self):
+        return (self.x, self.y)
+
+
+class Quant(Expr):
+    """ForAll / Exists / Cardinality(Comprehension) over processes; Exists over a value domain."""
+
+    def __init__(self, kind, var, body):
+        self.kind, self.var, self.body = kind, var, lift(body)  # kind: forall | exists | count | vint | vbool
+
+    def children(self):
+        return (self.body,)
+
+
+class Contains(Expr):
+    def __init__(self, comp, e):
+        self.comp, self.e = comp, lift(e)
+
+    def children(self):
+        return (self.e, self.comp.body)
+
+
+class Comprehension:
+    """P.filter(i => body): a set of processes (Comprehension in Formula.scala)."""
+
+    def __init__(self, var, body):
+        self.var, self.body = var, lift(body)
+
+    @property
+    def size(self):
+        return Quant("count", self.var, self.body)
+
+    def contains(self, e):
+        return Contains(self, e)
+
+
+def lift(v):
+    if isinstance(v, Expr):
+        return v
+    if isinstance(v, (bool, int)):
+        return Lit(v)
+    raise FormulaError(f"cannot use {v!r} in a Formula")
+
+
+def Some(e):
+    """Some(v) compared with an Option field (None is PSG_NONE32, so Some(v) == v)."""
+    return lift(e)
+
+
+def init(e):
+    """init(i.x): the value at check point 0 (FormulaExtractor `init`)."""
+    return _retag(e, TAG_INIT)
+
+
+def old(e):
+    """old(i.x): the value before the last round."""
+    return _retag(e, TAG_OLD)
+
+
+def _retag(e, tag):
+    if isinstance(e, Field):
+        return Field(e.f, e.proc, tag)
+    if isinstance(e, Un) and e.op in ("ISDEF", "NOT"):
+        return Un(e.op, _retag(e.x, tag))
+    raise FormulaError("init/old apply to a process field")
+
+
+def And(*xs):
+    out = lift(xs[0])
+    for x in xs[1:]:
+        out = out & x
+    return out
+
+
+def Or(*xs):
+    out = lift(xs[0])
+    for x in xs[1:]:
+        out = out | x
+    return out
+
+
+def Implies(a, b):
+    return lift(a).implies(b)
+
+
+class _P:
+    """The process domain (psync/Algorithm.scala `P`)."""
+
+    @staticmethod
+    def forall(fn: Callable):
+        v = Var("proc")
+        return Quant("forall", v, fn(v))
+
+    @staticmethod
+    def exists(fn: Callable):
+        v = Var("proc")
+        return Quant("exists", v, fn(v))
+
+    @staticmethod
+    def filter(fn: Callable):
+        v = Var("proc")
+        return Comprehension(v, fn(v))
+
+
+class _Domain:
+    """`new Domain[Int]` / `new Domain[Boolean]` (only `exists` is meaningful to check)."""
+
+    def __init__(self, kind):
+        self.kind = kind
+
+    def exists(self, fn: Callable):
+        v = Var(self.kind)
+        return Quant("vint" if self.kind == "int" else "vbool", v, fn(v))
+
+
+P = _P()
+V = _Domain("int")
+VB = _Domain("bool")
+n = NVal()
+r = RVal()
+coord = CoordVal()
+true = Lit(1)
+false = Lit(0)
+
+
+# --------------------------------------------------------------------------- Spec
+class Spec:
+    """psync/Specs.scala:8-16: safetyPredicate, invariants, roundInvariants, properties."""
+
+    def __init__(self, invariants: Sequence[Expr] = (), round_invariants: Sequence[Sequence[Expr]] = (),
+                 properties: Sequence[Tuple[str, Expr]] = (), safety_predicate: Optional[Expr] = None,
+                 phase_length: int = 1):
+        self.invariants = [lift(f) for f in invariants]
+        self.round_invariants = [[lift(f) for f in l] for l in round_invariants]
+        self.properties = [(name, lift(f)) for name, f in properties]
+        self.safety_predicate = None if safety_predicate is None else lift(safety_predicate)
+        self.phase_length = int(phase_length)
+
+
+class Program:
+    """A compiled Spec: psg_spec_program plus slot names."""
+
+    def __init__(self, code, slot_entry, slot_flags, term_entry, n_vars, slot_names, fields):
+        self.code, self.slot_entry, self.slot_flags = list(code), list(slot_entry), list(slot_flags)
+        self.term_entry, self.n_vars, self.slot_names, self.fields = term_entry, n_vars, list(slot_names), fields
+        self._keep = None
+
+    def to_c(self) -> abi.SpecProgram:
+        code = (C.c_int32 * len(self.code))(*self.code)
+        ent = (C.c_int32 * len(self.slot_entry))(*self.slot_entry)
+        flg = (C.c_int32 * len(self.slot_flags))(*self.slot_flags)
+        self._keep = (code, ent, flg)
+        p = abi.SpecProgram()
+        p.n_slots = len(self.slot_entry)
+        p.n_words = len(self.code)
+        p.code = C.cast(code, C.POINTER(C.c_int32))
+        p.slot_entry = C.cast(ent, C.POINTER(C.c_int32))
+        p.slot_flags = C.cast(flg, C.POINTER(C.c_int32))
+        p.term_entry = self.term_entry
+        p.n_vars = self.n_vars
+        return p
+
+
+# --------------------------------------------------------------------------- compiler
+def _word(op, a=0, b=0):
+    if not (-(1 << 15) <= b < (1 << 15)):
+        raise FormulaError("immediate out of range")
+    w = (OP[op] & 0xFF) | ((a & 0xFF) << 8) | ((b & 0xFFFF) << 16)
+    return w - (1 << 32) if w >= (1 << 31) else w
+
+
+def _walk(e):
+    yield e
+    for c in e.children():
+        yield from _walk(c)
+
+
+def _free_vars(e, bound=frozenset()):
+    """uids of variables used in e but bound outside it."""
+    out = set()
+    if isinstance(e, Var):
+        if e.uid not in bound:
+            out.add(e.uid)
+        return out
+    if isinstance(e, Quant):
+        return _free_vars(e.body, bound | {e.var.uid})
+    if isinstance(e, Contains):
+        return _free_vars(e.e, bound) | _free_vars(e.comp.body, bound | {e.comp.var.uid})
+    for c in e.children():
+        out |= _free_vars(c, bound)
+    return out
+
+
+def _strip(e):
+    return e  # `.get` is the identity on the int encoding
+
+
+def _uses_old(e):
+    return any(isinstance(x, Field) and x.tag == TAG_OLD for x in _walk(e))
+
+
+class _Compiler:
+    def __init__(self, fields_available=None):
+        self.code: List[int] = []
+        self.slot_of: Dict[int, int] = {}
+        self.max_slot = -1
+        self.fields_used = set()
+        self.fields_available = fields_available
+
+    def emit(self, w):
+        self.code.append(w)
+        return len(self.code) - 1
+
+    def bind(self, var, depth):
+        if depth >= MAX_VARS:
+            raise FormulaError(f"more than {MAX_VARS} nested bound variables")
+        self.slot_of[var.uid] = depth
+        self.max_slot = max(self.max_slot, depth)
+        return depth
+
+    def expr(self, e, depth, in_lane):
+        if isinstance(e, Lit):
+            if -(1 << 15) <= e.v < (1 << 15):
+                self.emit(_word("IMM", 0, e.v))
+            else:
+                self.emit(_word("IMM32"))
+                self.emit(e.v)
+        elif isinstance(e, NVal):
+            self.emit(_word("N"))
+        elif isinstance(e, RVal):
+            self.emit(_word("R"))
+        elif isinstance(e, CoordVal):
+            self.emit(_word("COORD"))
+        elif isinstance(e, Var):
+            if e.uid not in self.slot_of:
+                raise FormulaError("variable used outside its quantifier")
+            self.emit(_word("VAR", self.slot_of[e.uid]))
+        elif isinstance(e, Field):
+            if self.fields_available is not None and e.f not in self.fields_available:
+                raise FormulaError(f"field {e.f} is not part of this algorithm's state")
+            self.fields_used.add(e.f)
+            self.expr(e.proc, depth, in_lane)
+            self.emit(_word("FIELD", e.f, e.tag))
+        elif isinstance(e, Un):
+            self.expr(e.x, depth, in_lane)
+            self.emit(_word(e.op))
+        elif isinstance(e, Bin):
+            self.expr(e.x, depth, in_lane)
+            self.expr(e.y, depth, in_lane)
+            self.emit(_word(e.op))
+        elif isinstance(e, Contains):
+            # A.contains(e) == body of A with its variable bound to e
+            self.expr(e.e, depth, in_lane)
+            slot = self.bind(e.comp.var, depth)
+            self.emit(_word("BIND", slot))
+            self.expr(e.comp.body, depth + 1, in_lane)
+        elif isinstance(e, Quant):
+            self.quant(e, depth, in_lane)
+        else:
+            raise FormulaError(f"unsupported node {type(e).__name__}")
+
+    def quant(self, q, depth, in_lane):
+        slot = self.bind(q.var, depth)
+        lane_form = False
+        if q.kind in ("forall", "exists", "count"):
+            lane_form = not in_lane
+            base = {"forall": Q_FORALL_P, "exists": Q_EXISTS_P, "count": Q_COUNT_P}[q.kind]
+            kind = base + 3 if lane_form else base
+            head = [_word("QBEGIN", kind, slot)]
+        elif q.kind == "vbool":
+            head = [_word("QBEGIN", Q_EXISTS_VB, slot)]
+        else:  # vint: finitize over what v is compared with
+            exprs, fsets = self.witnesses(q)
+            for t in exprs:
+                self.expr(t, depth, in_lane)
+            head = [_word("QBEGIN", Q_EXISTS_VI, slot)]
+        at = self.emit(head[0])
+        end_at = self.emit(0)
+        if q.kind == "vint":
+            self.emit(len(exprs) | (len(fsets) << 16))
+            for f, tag in fsets:
+                self.fields_used.add(f)
+                self.emit(f | (tag << 8))
+        self.expr(q.body, depth + 1, in_lane or lane_form)
+        end = self.emit(_word("QEND"))
+        self.code[end_at] = end
+        return at
+
+    def witnesses(self, q):
+        """Candidate sources of V.exists(v => body): every term v is compared with."""
+        v = q.var.uid
+        inner = {x.var.uid for x in _walk(q.body) if isinstance(x, Quant)} | \
+                {x.comp.var.uid for x in _walk(q.body) if isinstance(x, Contains)}
+        exprs, fsets = [], []
+        seen_cmp = set()
+        for x in _walk(q.body):
+            if isinstance(x, Bin) and x.op in ("EQ", "NE", "LT", "LE", "GT", "GE"):
+                for a, b in ((x.x, x.y), (x.y, x.x)):
+                    if isinstance(a, Var) and a.uid == v:
+                        if v in _free_vars(b):
+                            raise FormulaError("V.exists variable compared with a term containing itself")
+                        t = _strip(b)
+                        if isinstance(t, Field):
+                            key = (t.f, t.tag)
+                            if key not in fsets:
+                                fsets.append(key)
+                        elif not (_free_vars(t) & inner):
+                            exprs.append(t)
+                        else:
+                            raise FormulaError("V.exists witness term depends on an inner bound variable "
+                                               "and is not a process field")
+                        seen_cmp.add(id(a))
+        for x in _walk(q.body):
+            if isinstance(x, Var) and x.uid == v and id(x) not in seen_cmp:
+                raise FormulaError("a V.exists variable may only appear directly in comparisons")
+        return exprs, fsets
+
+    def root(self, e):
+        at = len(self.code)
+        self.expr(e, 0, False)
+        self.emit(_word("HALT"))
+        return at
+
+
+def _rinv_guard(spec: Spec) -> Optional[Expr]:
+    """(r % L == j) ==> roundInvariants(j-1)(0) for j = 1..L-1 (Verifier.scala:133-141)."""
+    L = spec.phase_length
+    parts = []
+    for j in range(1, L):
+        if j - 1 < len(spec.round_invariants) and spec.round_invariants[j - 1]:
+            parts.append(((r % L) == j).implies(spec.round_invariants[j - 1][0]))
+    return And(*parts) if parts else None
+
+
+def compile_spec(spec: Spec, alg: Optional[int] = None) -> Program:
+    comp = _Compiler(ALG_FIELDS.get(alg) if alg is not None else None)
+    names, entries, flags = [], [], []
+    guard = _rinv_guard(spec)
+    invs = [inv if guard is None else (inv & guard) for inv in spec.invariants]
+    if invs:
+        names.append("Safety")
+        entries.append(comp.root(Or(*invs)))
+        flags.append(0)
+        for k, inv in enumerate(invs):
+            names.append(f"Invariant{k}")
+            entries.append(comp.root(inv))
+            flags.append(0)
+    term = -1
+    for name, f in spec.properties:
+        if name == "Termination":
+            term = comp.root(f)
+            continue
+        names.append(name)
+        entries.append(comp.root(f))
+        flags.append(SPEC_RELATIONAL if _uses_old(f) else 0)
+    if spec.safety_predicate is not None:
+        names.append("SafetyPredicate")
+        entries.append(comp.root(spec.safety_predicate))
+        flags.append(SPEC_RELATIONAL if _uses_old(spec.safety_predicate) else 0)
+    if not entries:
+        raise FormulaError("a Spec needs at least one invariant, property or safety predicate")
+    if len(entries) > abi.PSG_MAX_CHECKS:
+        raise FormulaError(f"more than {abi.PSG_MAX_CHECKS} check slots")
+    return Program(comp.code, entries, flags, term, comp.max_slot + 1, names, comp.fields_used)
+
+
+# --------------------------------------------------------------------------- the reference specs, restated
+def otr_spec() -> Spec:
+    """example/Otr.scala:95-120."""
+    def A(v): return P.filter(lambda i: i.x == v)
+    keep_init = P.forall(lambda i: P.exists(lambda j1: i.x == init(j1.x)))
+    inv0 = (P.forall(lambda i: ~i.decided)
+            | V.exists(lambda v: (A(v).size > 2 * n // 3)
+                       & P.forall(lambda i: i.decided.implies(i.decision == v)))) & keep_init
+    inv1 = V.exists(lambda v: (A(v).size == n)
+                    & P.forall(lambda i: i.decided.implies(i.decision == v))) & keep_init
+    inv2 = P.exists(lambda j: P.forall(lambda i: i.decided & (i.decision == init(j.x))))
+    return Spec([inv0, inv1, inv2], properties=_consensus_properties())
+
+
+def _consensus_properties():
+    return [
+        ("Termination", P.forall(lambda i: i.decided)),
+        ("Agreement", P.forall(lambda i: P.forall(lambda j: (i.decided & j.decided).implies(
+            i.decision == j.decision)))),
+        ("Validity", P.forall(lambda i: i.decided.implies(P.exists(lambda j: init(j.x) == i.decision)))),
+        ("Integrity", P.exists(lambda j: P.forall(lambda i: i.decided.implies(i.decision == init(j.x))))),
+        ("Irrevocability", P.forall(lambda i: old(i.decided).implies(
+            i.decided & (old(i.decision) == i.decision)))),
+    ]
+
+
+def otr2_spec() -> Spec:
+    """example/Otr2.scala:71-96 (decision: Option[Int])."""
+    def A(v): return P.filter(lambda i: i.x == v)
+    def all_dec(v): return P.forall(lambda i: i.decision.isDefined.implies(i.decision.get == v))
+    inv0 = P.forall(lambda i: ~i.decision.isEmpty) | V.exists(lambda v: (A(v).size > 2 * n // 3) & all_dec(v))
+    inv1 = V.exists(lambda v: (A(v).size == n) & all_dec(v))
+    inv2 = V.exists(lambda v: all_dec(v))
+    props = [
+        ("Termination", P.forall(lambda i: i.decision.isDefined)),
+        ("Agreement", P.forall(lambda i: P.forall(lambda j: (i.decision.isDefined & j.decision.isDefined).implies(
+            i.decision == j.decision)))),
+        ("Validity", P.forall(lambda i: i.decision.isDefined.implies(
+            P.exists(lambda j: init(j.x) == i.decision.get)))),
+        ("Integrity", P.exists(lambda j: P.forall(lambda i: i.decision.isDefined.implies(
+            i.decision.get == init(j.x))))),
+        ("Irrevocability", P.forall(lambda i: old(i.decision).isDefined.implies(old(i.decision) == i.decision))),
+    ]
+    return Spec([inv0, inv1, inv2], properties=props)
+
+
+def lv_spec() -> Spec:
+    """example/LastVoting.scala:19-70."""
+    no_decision = P.forall(lambda i: ~i.decided & ~i.ready)
+
+    def majority_body(v, t):
+        A = P.filter(lambda i: i.ts >= t)
+        return ((A.size > n // 2) & (r > 0) & (t <= r // 4)
+                & P.forall(lambda i: A.contains(i).implies(i.x == v)
+                           & i.decided.implies(i.decision == v)
+                           & i.commit.implies(i.vote == v)
+                           & i.ready.implies(i.vote == v)
+                           & (i.ts == r // 4).implies(coord.commit)))
+
+    majority = V.exists(lambda v: V.exists(lambda t: majority_body(v, t)))
+    keep_init = P.forall(lambda i: P.exists(lambda j1: i.x == init(j1.x)))
+    safety_inv = And(keep_init, Or(no_decision, majority))
+    inv1 = P.exists(lambda j: P.forall(lambda i: i.decided & (i.decision == init(j.x))))
+    rinv = [
+        [true, P.exists(lambda i: i.commit)],
+        [true, P.exists(lambda i: i.commit & P.forall(lambda j: (j.ts == r // 4) & (j.x == i.vote)))],
+        [true, P.exists(lambda i: i.commit & i.ready & P.forall(lambda j: (j.ts == r // 4) & (j.x == i.vote)))],
+    ]
+    return Spec([safety_inv, inv1], rinv, _consensus_properties(), phase_length=4)
+
+
+def benor_spec() -> Spec:
+    """example/BenOr.scala:91-115 (V = Domain[Boolean])."""
+    inv0 = (P.forall(lambda i: ~i.decided & ~i.canDecide)
+            | VB.exists(lambda v: (P.filter(lambda i: i.x == v).size > n // 2)
+                        & P.forall(lambda i: i.decided.implies(i.decision == v)
+                                   & i.vote.isDefined.implies(i.vote == Some(v)))))
+    rinv = [[P.forall(lambda p: p.vote.isDefined.implies(P.filter(lambda i: i.x == p.vote.get).size > n // 2))]]
+    props = [
+        ("Agreement", P.forall(lambda i: P.forall(lambda j: (i.decided & j.decided).implies(
+            i.decision == j.decision)))),
+        ("Irrevocability", P.forall(lambda i: old(i.decided).implies(i.decided & (old(i.decision) == i.decision)))),
+        ("Termination", P.forall(lambda i: i.decided)),
+    ]
+    return Spec([inv0], rinv, props, safety_predicate=P.forall(lambda p: p.HO.size > n // 2), phase_length=2)
+
+
+REFERENCE_SPECS = {
+    abi.PSG_ALG_OTR: otr_spec,
+    abi.PSG_ALG_OTR2: otr2_spec,
+    abi.PSG_ALG_LAST_VOTING: lv_spec,
+    abi.PSG_ALG_BENOR: benor_spec,
+}

@@ -23,6 +23,7 @@ EXPORTED_SYMBOLS = [
     "psg_create", "psg_load_inputs", "psg_run_batch", "psg_copy_decisions",
     "psg_fetch_instances", "psg_last_error", "psg_destroy", "psg_create_error",
     "psg_selftest_map_head", "psg_load_inputs_f64", "psg_copy_decisions_f64", "psg_fetch_instances_f64",
+    "psg_run_batch_spec",
 ]
 
 
@@ -65,6 +66,8 @@ def load():
     L.psg_fetch_instances_f64.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t,
                                           C.POINTER(abi.InstanceSummary), C.POINTER(abi.ProcessRecord),
                                           C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.psg_run_batch_spec.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(abi.SpecProgram),
+                                     C.POINTER(abi.Summary), C.POINTER(abi.InstanceSummary)]
     L.psg_selftest_map_head.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
                                         C.POINTER(C.c_int32)]
     _lib = L
@@ -111,6 +114,15 @@ class Context:
         s = abi.Summary()
         pi = (abi.InstanceSummary * count)() if per_instance else None
         self._check(load().psg_run_batch(self._h, inst_begin, count, C.byref(s), pi))
+        self._last_count = count
+        return s, (list(pi) if pi is not None else None)
+
+    def run_batch_spec(self, inst_begin, count, program, per_instance=False):
+        """psg_run_batch_spec with a compiled Spec (round_amd.formula.Program)."""
+        s = abi.Summary()
+        pi = (abi.InstanceSummary * count)() if per_instance else None
+        cp = program.to_c()
+        self._check(load().psg_run_batch_spec(self._h, inst_begin, count, C.byref(cp), C.byref(s), pi))
         self._last_count = count
         return s, (list(pi) if pi is not None else None)
 

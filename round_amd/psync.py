@@ -266,6 +266,16 @@ class BatchResult:
         return {names[i]: self.summary.fail_count[i] for i in self.alg.violation_slots}
 
 
+class SpecResult:
+    """Result of a batch checked against a user Spec: counts per compiled slot."""
+
+    def __init__(self, slot_names, rounds, summary, per_instance=None):
+        self.slot_names, self.rounds, self.summary, self.per_instance = slot_names, rounds, summary, per_instance
+
+    def fail_count(self):
+        return {name: self.summary.fail_count[i] for i, name in enumerate(self.slot_names)}
+
+
 class GpuRound:
     """Lockstep HO executor on one MI355X — the drop-in for in-JVM execution.
 
@@ -298,6 +308,14 @@ class GpuRound:
     def run(self, inst_begin: int, count: int, per_instance: bool = False) -> BatchResult:
         s, pi = self._ctx.run_batch(inst_begin, count, per_instance)
         return BatchResult(self.alg, self.cfg.rounds, s, pi)
+
+    def run_spec(self, inst_begin: int, count: int, spec, per_instance: bool = False):
+        """Run with a user Spec (round_amd.formula.Spec or a compiled Program) instead
+        of the built-in checks. Returns (BatchResult-like summary, slot names)."""
+        from . import formula
+        prog = spec if isinstance(spec, formula.Program) else formula.compile_spec(spec, self.alg.alg_id)
+        s, pi = self._ctx.run_batch_spec(inst_begin, count, prog, per_instance)
+        return SpecResult(prog.slot_names, self.cfg.rounds, s, pi)
 
     def decisions(self):
         return self._ctx.copy_decisions()

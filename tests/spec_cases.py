@@ -1,0 +1,62 @@
+"""Custom Spec programs shared by the CPU (test_formula.py) and GPU (test_gpu_spec.py) tests."""
+from round_amd import formula as F, psync
+
+P, V, VB, n, r, init, old = F.P, F.V, F.VB, F.n, F.r, F.init, F.old
+H = psync.HOSchedule
+
+
+def uniform_agreement():
+    return F.Spec(properties=[
+        ("Termination", P.forall(lambda i: i.decided)),
+        ("UniformAgreement", P.forall(lambda i: P.forall(lambda j: (i.decided & j.decided).implies(
+            i.decision == j.decision)))),
+        ("XNonIncreasing", P.forall(lambda i: i.x <= old(i.x))),
+        ("XInitial", P.forall(lambda i: P.exists(lambda j: i.x == init(j.x)))),
+    ])
+
+
+def at_most_two_decisions():
+    """|{decisions}| <= 2 as two nested V.exists over Int."""
+    return F.Spec(properties=[
+        ("TwoSet", V.exists(lambda v1: V.exists(lambda v2: P.forall(lambda i: i.decided.implies(
+            (i.decision == v1) | (i.decision == v2)))))),
+        ("DecidedCount", P.filter(lambda i: i.decided).size <= n),
+    ])
+
+
+def lv_custom():
+    return F.Spec(
+        invariants=[P.forall(lambda i: i.commit.implies(P.exists(lambda j: j.x == i.vote)))],
+        properties=[
+            ("TsBound", P.forall(lambda i: i.ts <= r // 4)),
+            ("PhaseEnd", ((r % 4) == 0).implies(P.forall(lambda i: ~i.ready))),
+            ("WitnessExpr", V.exists(lambda v: (v == r // 4 + 1) & (v > 0))),
+            ("CoordVote", F.coord.commit.implies(P.exists(lambda j: j.x == F.coord.vote) | (r >= 0))),
+        ])
+
+
+def benor_custom():
+    return F.Spec(
+        properties=[
+            ("MajorityHO", P.forall(lambda p: p.HO.size > n // 2)),
+            ("VoteIsX", P.forall(lambda i: i.vote.isDefined.implies(
+                VB.exists(lambda b: (i.vote == F.Some(b)) & (P.filter(lambda j: j.x == b).size >= 0))))),
+            ("Termination", P.forall(lambda i: i.decided)),
+        ])
+
+
+# (id, algorithm, n, make_config kwargs, spec factory)
+CUSTOM = [
+    ("fm-n12", psync.FloodMin(2), 12, dict(value_range=8, schedule=H(drop_log2=0, good_round=0.0, crash_fmax=3)),
+     uniform_agreement),
+    ("fm-n100", psync.FloodMin(2), 100, dict(value_range=8, schedule=H(drop_log2=0, good_round=0.0, crash_fmax=3)),
+     uniform_agreement),
+    ("kses-n16", psync.KSetEarlyStopping(4, 2), 16, dict(value_range=6), at_most_two_decisions),
+    ("kses-n70", psync.KSetEarlyStopping(4, 2), 70, dict(value_range=6), at_most_two_decisions),
+    ("kset-n16", psync.KSetAgreement(2), 16, dict(value_range=6), at_most_two_decisions),
+    ("lv-n8", psync.LastVoting(), 8, dict(value_range=4, schedule=H(drop_log2=1, good_round=0.0, crash_fmax=3)),
+     lv_custom),
+    ("slv-n16", psync.ShortLastVoting(), 16, dict(value_range=4), uniform_agreement),
+    ("benor-n8", psync.BenOr(), 8, {}, benor_custom),
+    ("otr2-n12", psync.OTR2(), 12, dict(value_range=4), uniform_agreement),
+]

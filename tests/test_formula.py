@@ -1,0 +1,80 @@
+"""Generic Spec programs (round_amd/formula.py -> include/psg.h bytecode), CPU side.
+
+1. The reference Specs restated in the Python DSL, compiled and run by the CPU
+   interpreter (oracle_vm_run) over oracle traces, reproduce the oracle's own
+   checker (hand-lowered == Formula-tree interpreter) per instance.
+2. Custom specs: compiled program == direct recursive evaluation with a
+   brute-forced V.exists domain (tests/formula_ref.py).
+3. Compiler errors for shapes the finitization cannot cover exactly.
+"""
+import pytest
+
+from round_amd import abi, formula as F, psync
+
+import formula_ref
+import spec_cases
+
+H = psync.HOSchedule
+
+
+@pytest.mark.parametrize("alg,n,kw", [
+    (psync.OTR(), 8, {}),
+    (psync.OTR(), 16, dict(value_range=3, schedule=H(drop_log2=1))),
+    (psync.OTR(variant=1), 8, dict(schedule=H(drop_log2=1, good_round=0.0))),
+    (psync.OTR2(), 10, {}),
+    (psync.LastVoting(), 8, dict(value_range=3, schedule=H(drop_log2=1, good_round=0.0, crash_fmax=3))),
+    (psync.LastVoting(variant=1), 6, dict(value_range=5)),
+    (psync.BenOr(), 8, {}),
+    (psync.BenOr(variant=1), 6, {}),
+], ids=lambda v: getattr(v, "class_name", None) or None)
+def test_reference_specs_compile_to_the_oracle_checker(alg, n, kw, oracle_mod):
+    cfg = psync.make_config(alg, n, seed=13, **kw)
+    prog = F.compile_spec(F.REFERENCE_SPECS[alg.alg_id](), alg.alg_id)
+    assert prog.slot_names == abi.CHECK_NAMES[alg.alg_id]
+    cnt = 200
+    tr = oracle_mod.trace(cfg, 0, cnt)
+    ff, tm = oracle_mod.vm_run(prog, tr, cnt, n, cfg.rounds)
+    _, pi, _ = oracle_mod.run(cfg, 0, cnt, per_instance=True, threads=8)
+    k = len(prog.slot_names)
+    for i in range(cnt):
+        assert ff[i] == list(pi[i].first_fail)[:k] and tm[i] == pi[i].term_round, i
+
+
+@pytest.mark.parametrize("cid,alg,n,kw,mk", [c for c in spec_cases.CUSTOM if c[2] <= 16],
+                         ids=[c[0] for c in spec_cases.CUSTOM if c[2] <= 16])
+def test_custom_specs_match_direct_evaluation(cid, alg, n, kw, mk, oracle_mod):
+    cfg = psync.make_config(alg, n, seed=17, **kw)
+    spec = mk()
+    prog = F.compile_spec(spec, alg.alg_id)
+    cnt = 12
+    tr = oracle_mod.trace(cfg, 0, cnt)
+    ff, tm = oracle_mod.vm_run(prog, tr, cnt, n, cfg.rounds)
+    rf, rt = formula_ref.evaluate(spec, tr, cnt, n, cfg.rounds)
+    assert ff == rf and tm == rt
+
+
+def test_custom_specs_find_violations(oracle_mod):
+    """A false property is reported at the first check point it fails."""
+    spec = F.Spec(properties=[("NobodyDecides", F.P.forall(lambda i: ~i.decided))])
+    cfg = psync.make_config(psync.FloodMin(1), 6, seed=3, value_range=5)
+    prog = F.compile_spec(spec, abi.PSG_ALG_FLOODMIN)
+    tr = oracle_mod.trace(cfg, 0, 10)
+    ff, _ = oracle_mod.vm_run(prog, tr, 10, 6, cfg.rounds)
+    assert all(f == [3] for f in ff)  # FloodMin(f=1) decides in round k = 2 (first r > f): check point 3
+
+
+def test_compiler_rejects_inexact_witness_shapes():
+    P, V = F.P, F.V
+    with pytest.raises(F.FormulaError):  # v used in arithmetic
+        F.compile_spec(F.Spec([V.exists(lambda v: P.forall(lambda i: i.x + 1 == v * 2))]))
+    with pytest.raises(F.FormulaError):  # field of the wrong algorithm
+        F.compile_spec(F.Spec([P.forall(lambda i: i.ts >= 0)]), abi.PSG_ALG_OTR)
+    with pytest.raises(F.FormulaError):  # Python boolean operators on formulas
+        F.compile_spec(F.Spec([P.forall(lambda i: i.decided and i.x > 0)]))
+
+
+def test_program_layout():
+    prog = F.compile_spec(F.otr_spec(), abi.PSG_ALG_OTR)
+    assert prog.term_entry >= 0 and prog.n_vars <= 16
+    assert prog.slot_flags == [0, 0, 0, 0, 0, 0, 0, F.SPEC_RELATIONAL]
+    assert all(prog.code[e - 1] & 0xFF == 0 or e == 0 for e in prog.slot_entry)  # each root follows a HALT
