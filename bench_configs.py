@@ -45,6 +45,12 @@ def configs(scale):
     out.append(("W2_slv_n64", psync.ShortLastVoting(), 64, int(12_500_000 * s), {}, 40))
     out.append(("W2_kset_es_n256_t64_k2", psync.KSetEarlyStopping(64, 2), 256, int(1_000_000 * s), {}, 32))
     out.append(("W2_epsilon_n64_f5", psync.EpsilonConsensus(5, 1e-6), 64, int(1_000_000 * s), {}, 66))
+    # generic Spec programs: the reference Specs compiled from the Formula
+    # DSL and interpreted on the device over the traced states (psg_run_batch_spec)
+    from round_amd import formula
+    out.append(("G1_otr_n64_specprog", psync.OTR(), 64, int(1_000_000 * s), dict(value_range=64), 24,
+                formula.otr_spec))
+    out.append(("G1_lv_n64_specprog", psync.LastVoting(), 64, int(250_000 * s), {}, 42, formula.lv_spec))
     return out
 
 
@@ -65,14 +71,17 @@ def main():
     if launched:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
     results = []
-    for name, alg, n, I, kw, balg in configs(args.scale):
+    for row in configs(args.scale):
+        name, alg, n, I, kw, balg = row[:6]
+        spec = row[6]() if len(row) > 6 else None
         if args.only and not any(name.startswith(p) for p in args.only.split(",")):
             continue
         g = psync.GpuRound(alg, n, seed=7, device=dev, batch_capacity=I, **kw)
         begin, _ = rdist.shard(rank, world, I)
         g.load_inputs(begin, I)
+        step = (lambda: g.run(begin, I)) if spec is None else (lambda: g.run_spec(begin, I, spec))
         for _ in range(args.warmup):
-            g.run(begin, I)
+            step()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -80,7 +89,7 @@ def main():
         kns = 0
         last = None
         for _ in range(args.steps):
-            last = g.run(begin, I)
+            last = step()
             kns += last.summary.kernel_ns
         torch.cuda.synchronize()
         if world > 1:
@@ -104,6 +113,7 @@ def main():
                              "frac": pr_launch * balg / kern / 1e9 / HBM_PEAK_GBS},
                 "violations": psync.BatchResult(alg, R, tot).violations(),
                 "fail_count": psync.BatchResult(alg, R, tot).as_dict()["fail_count"],
+                "spec": "compiled Formula program (psg_run_batch_spec)" if spec is not None else "built-in",
                 "terminated_fraction": done / max(1, tot.instances),
                 "mean_termination_round": (sum(i * c for i, c in enumerate(th[:-1])) / done) if done else None,
                 "term_hist": th,
