@@ -22,6 +22,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402  (first: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
+from round_amd import abi  # noqa: E402
 from round_amd import dist as rdist  # noqa: E402
 from round_amd import psync  # noqa: E402
 
@@ -49,8 +50,14 @@ def configs(scale):
     # DSL and interpreted on the device over the traced states (psg_run_batch_spec)
     from round_amd import formula
     out.append(("G1_otr_n64_specprog", psync.OTR(), 64, int(1_000_000 * s), dict(value_range=64), 24,
-                formula.otr_spec))
-    out.append(("G1_lv_n64_specprog", psync.LastVoting(), 64, int(250_000 * s), {}, 42, formula.lv_spec))
+                lambda: formula.compile_spec(formula.otr_spec(), abi.PSG_ALG_OTR)))
+    out.append(("G1_lv_n64_specprog", psync.LastVoting(), 64, int(250_000 * s), {}, 42,
+                lambda: formula.compile_spec(formula.lv_spec(), abi.PSG_ALG_LAST_VOTING)))
+    # the same Specs lowered to native wave code (formula.compile_native)
+    out.append(("G1_otr_n64_native", psync.OTR(), 64, int(10_000_000 * s), dict(value_range=64), 24,
+                lambda: formula.compile_native(formula.otr_spec(), abi.PSG_ALG_OTR)))
+    out.append(("G1_lv_n64_native", psync.LastVoting(), 64, int(2_500_000 * s), {}, 42,
+                lambda: formula.compile_native(formula.lv_spec(), abi.PSG_ALG_LAST_VOTING)))
     return out
 
 
@@ -113,7 +120,9 @@ def main():
                              "frac": pr_launch * balg / kern / 1e9 / HBM_PEAK_GBS},
                 "violations": psync.BatchResult(alg, R, tot).violations(),
                 "fail_count": psync.BatchResult(alg, R, tot).as_dict()["fail_count"],
-                "spec": "compiled Formula program (psg_run_batch_spec)" if spec is not None else "built-in",
+                "spec": ("built-in" if spec is None else
+                         "native lowered Formula (psg_run_batch_spec)" if spec.module_path else
+                         "Formula bytecode interpreter (psg_run_batch_spec)"),
                 "terminated_fraction": done / max(1, tot.instances),
                 "mean_termination_round": (sum(i * c for i, c in enumerate(th[:-1])) / done) if done else None,
                 "term_hist": th,

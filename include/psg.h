@@ -222,6 +222,9 @@ typedef struct psg_spec_program {
   const int32_t* slot_flags; /* [n_slots] PSG_SPEC_* */
   int32_t term_entry;        /* pc of the Termination expression, -1 for none */
   int32_t n_vars;            /* bound variables used, <= 16 */
+  const char* module_path;   /* NULL: interpret the bytecode; else a gfx950 code object with kernels
+                                psg_spec_native_w1..w4 (the same Spec lowered to wave code by
+                                round_amd/formula.py compile_native), launched instead */
 } psg_spec_program;
 
 typedef struct psg_ctx psg_ctx;

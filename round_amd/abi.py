@@ -198,4 +198,5 @@ class SpecProgram(C.Structure):
         ("slot_flags", C.POINTER(C.c_int32)),
         ("term_entry", C.c_int32),
         ("n_vars", C.c_int32),
+        ("module_path", C.c_char_p),
     ]

@@ -61,6 +61,9 @@ struct psg_ctx {
   int32_t* d_vm_err = nullptr;
   int32_t* d_prog = nullptr;     // code | slot_entry | slot_flags
   size_t prog_cap = 0;
+  std::string module_path;       // native Spec code object currently loaded
+  hipModule_t module = nullptr;
+  hipFunction_t native_fn = nullptr;
   bool staged = false;
   uint64_t staged_begin = 0, staged_count = 0;
   int32_t* d_dec = nullptr;
@@ -584,6 +587,18 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
   if (!c->d_vm_err) HIPCHK(c, hipMalloc(&c->d_vm_err, sizeof(int32_t)));
   HIPCHK(c, hipMemsetAsync(c->d_vm_err, 0, sizeof(int32_t), c->stream));
   const bool staged = c->staged && c->staged_begin == inst_begin && c->staged_count == count;
+  // native lowering of the same Spec (round_amd/formula.py compile_native), if given
+  const bool native = prog->module_path != nullptr;
+  if (native && c->module_path != prog->module_path) {
+    if (c->module) (void)hipModuleUnload(c->module);
+    c->module = nullptr;
+    c->native_fn = nullptr;
+    c->module_path.clear();
+    HIPCHK(c, hipModuleLoad(&c->module, prog->module_path));
+    const std::string name = "psg_spec_native_w" + std::to_string(c->W);
+    HIPCHK(c, hipModuleGetFunction(&c->native_fn, c->module, name.c_str()));
+    c->module_path = prog->module_path;
+  }
   psg_summary acc;
   std::memset(&acc, 0, sizeof(acc));
   int vm_grid = 0;
@@ -618,7 +633,15 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
     v.err = c->d_vm_err;
     HIPCHK(c, hipMemsetAsync(c->d_vm_counters, 0, sizeof(unsigned long long) * NCOUNTERS, c->stream));
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, launch_spec_vm(v, (int)std::min<uint64_t>(m_cnt, (uint64_t)vm_grid), c->stream));
+    if (native) {
+      const int G = groups_per_block(c->W);
+      const unsigned grid = (unsigned)std::min<uint64_t>((m_cnt + G - 1) / G, (uint64_t)vm_grid);
+      const unsigned threads = c->W == 1 ? 256u : 64u * (unsigned)c->W;
+      void* params[] = {&v};
+      HIPCHK(c, hipModuleLaunchKernel(c->native_fn, grid, 1, 1, threads, 1, 1, 0, c->stream, params, nullptr));
+    } else {
+      HIPCHK(c, launch_spec_vm(v, (int)std::min<uint64_t>(m_cnt, (uint64_t)vm_grid), c->stream));
+    }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     unsigned long long host[NCOUNTERS];
     HIPCHK(c, hipMemcpyAsync(host, c->d_vm_counters, sizeof(host), hipMemcpyDeviceToHost, c->stream));
@@ -740,6 +763,7 @@ void psg_destroy(psg_ctx* c) {
   if (c->d_vm_counters) (void)hipFree(c->d_vm_counters);
   if (c->d_vm_err) (void)hipFree(c->d_vm_err);
   if (c->d_prog) (void)hipFree(c->d_prog);
+  if (c->module) (void)hipModuleUnload(c->module);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -344,6 +344,7 @@ class Program:
     def __init__(self, code, slot_entry, slot_flags, term_entry, n_vars, slot_names, fields):
         self.code, self.slot_entry, self.slot_flags = list(code), list(slot_entry), list(slot_flags)
         self.term_entry, self.n_vars, self.slot_names, self.fields = term_entry, n_vars, list(slot_names), fields
+        self.module_path = None  # native code object (compile_native) or None: bytecode interpreter
         self._keep = None
 
     def to_c(self) -> abi.SpecProgram:
@@ -359,6 +360,7 @@ class Program:
         p.slot_flags = C.cast(flg, C.POINTER(C.c_int32))
         p.term_entry = self.term_entry
         p.n_vars = self.n_vars
+        p.module_path = self.module_path.encode() if self.module_path else None
         return p
 
 
@@ -658,3 +660,205 @@ REFERENCE_SPECS = {
     abi.PSG_ALG_LAST_VOTING: lv_spec,
     abi.PSG_ALG_BENOR: benor_spec,
 }
+
+
+# --------------------------------------------------------------------------- native lowering (HIP)
+_CSRC = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "csrc")
+_INCLUDE = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(_CSRC)), "include")
+CACHE_DIR = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(_CSRC)),
+                                        "build", "spec")
+
+
+def _c_int(v):
+    return "(-2147483647 - 1)" if v == -(1 << 31) else f"((int32_t){v})"
+
+
+class _Gen:
+    """Formula tree -> C++ expression over psg_spec_native.hpp (template parameter W)."""
+
+    BIN = {"AND": "(int32_t)((({x}) != 0) & (({y}) != 0))", "OR": "(int32_t)((({x}) != 0) | (({y}) != 0))",
+           "IMPL": "(int32_t)((({x}) == 0) | (({y}) != 0))", "EQ": "(int32_t)(({x}) == ({y}))",
+           "NE": "(int32_t)(({x}) != ({y}))", "LT": "(int32_t)(({x}) < ({y}))", "LE": "(int32_t)(({x}) <= ({y}))",
+           "GT": "(int32_t)(({x}) > ({y}))", "GE": "(int32_t)(({x}) >= ({y}))", "ADD": "spec::iadd({x}, {y})",
+           "SUB": "spec::isub({x}, {y})", "MUL": "spec::imul({x}, {y})", "DIV": "spec::idiv({x}, {y})",
+           "MOD": "spec::imod({x}, {y})"}
+
+    def __init__(self, fields_available=None):
+        self.names = {}       # var uid -> (c name, per-lane?, lane-bound pid?)
+        self.k = itertools.count()
+        self.fields = set()
+        self.tags = set()
+        self.fields_available = fields_available
+        self.max_vi = 0
+
+    def gen(self, e, in_lane, vi_depth):
+        """(C++ expression, depends on the lane)."""
+        if isinstance(e, Lit):
+            return _c_int(e.v), False
+        if isinstance(e, NVal):
+            return "x.n", False
+        if isinstance(e, RVal):
+            return "x.r", False
+        if isinstance(e, CoordVal):
+            return "((x.r / 4) % x.n)", False
+        if isinstance(e, Var):
+            if e.uid not in self.names:
+                raise FormulaError("variable used outside its quantifier")
+            name, lane, _ = self.names[e.uid]
+            return name, lane
+        if isinstance(e, Field):
+            if self.fields_available is not None and e.f not in self.fields_available:
+                raise FormulaError(f"field {e.f} is not part of this algorithm's state")
+            self.fields.add(e.f)
+            self.tags.add(e.tag)
+            if isinstance(e.proc, Var) and self.names.get(e.proc.uid, (None, False, False))[2]:
+                return f"x.own({e.tag}, {e.f})", True  # the lane's own process
+            p, lane = self.gen(e.proc, in_lane, vi_depth)
+            fn = "fld_g" if lane else "fld_u"
+            return f"spec::{fn}<W>(x, {e.tag}, {e.f}, {p})", lane
+        if isinstance(e, Un):
+            a, lane = self.gen(e.x, in_lane, vi_depth)
+            if e.op == "NOT":
+                return f"(int32_t)(({a}) == 0)", lane
+            if e.op == "NEG":
+                return f"spec::isub(0, {a})", lane
+            return f"(int32_t)(({a}) != (-2147483647 - 1))", lane
+        if isinstance(e, Bin):
+            a, la = self.gen(e.x, in_lane, vi_depth)
+            b, lb = self.gen(e.y, in_lane, vi_depth)
+            return self.BIN[e.op].format(x=a, y=b), la or lb
+        if isinstance(e, Contains):
+            val, lane = self.gen(e.e, in_lane, vi_depth)
+            v = f"b{next(self.k)}"
+            self.names[e.comp.var.uid] = (v, lane, False)
+            body, lb = self.gen(e.comp.body, in_lane, vi_depth)
+            return f"([&](int32_t {v}) -> int32_t {{ return {body}; }})({val})", lane or lb
+        if isinstance(e, Quant):
+            return self.quant(e, in_lane, vi_depth)
+        raise FormulaError(f"unsupported node {type(e).__name__}")
+
+    def quant(self, q, in_lane, vi_depth):
+        v = f"v{next(self.k)}"
+        if q.kind in ("forall", "exists", "count"):
+            if not in_lane:
+                self.names[q.var.uid] = (v, True, True)
+                body, _ = self.gen(q.body, True, vi_depth)
+                fn = {"forall": "forall_lane", "exists": "exists_lane", "count": "count_lane"}[q.kind]
+                return f"spec::{fn}<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", False
+            self.names[q.var.uid] = (v, False, False)
+            body, lane = self.gen(q.body, in_lane, vi_depth)
+            fn = {"forall": "forall_ser", "exists": "exists_ser", "count": "count_ser"}[q.kind]
+            return f"spec::{fn}<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", lane
+        self.names[q.var.uid] = (v, False, False)
+        if q.kind == "vbool":
+            body, lane = self.gen(q.body, in_lane, vi_depth)
+            return f"spec::exists_bool<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", lane
+        exprs, fsets = _Compiler.witnesses(_Compiler(), q)
+        evs = []
+        for t in exprs:
+            c, _ = self.gen(t, in_lane, vi_depth)
+            evs.append(c)
+        for f, tag in fsets:
+            self.fields.add(f)
+            self.tags.add(tag)
+        self.max_vi = max(self.max_vi, vi_depth + 1)
+        body, lane = self.gen(q.body, in_lane, vi_depth + 1)
+        ne, nf = len(evs), len(fsets)
+        ev = ", ".join(evs) if evs else "0"
+        fs = ", ".join(str(f | (t << 8)) for f, t in fsets) if fsets else "0"
+        return (f"([&]() -> int32_t {{ const int32_t ev_[{max(ne, 1)}] = {{{ev}}}; "
+                f"const int32_t fs_[{max(nf, 1)}] = {{{fs}}}; "
+                f"return spec::exists_int<W, {ne}, {nf}>(x, ev_, fs_, scratch + {vi_depth} * 64 * W, "
+                f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); }})()"), True
+
+
+def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
+    """HIP source of the native checker of `spec` (+ the bytecode Program it replaces)."""
+    prog = compile_spec(spec, alg)
+    gen = _Gen(ALG_FIELDS.get(alg) if alg is not None else None)
+    guard = _rinv_guard(spec)
+    invs = [inv if guard is None else (inv & guard) for inv in spec.invariants]
+    lines = []
+    slot = 0
+    if invs:
+        for k, inv in enumerate(invs):
+            c, _ = gen.gen(inv, False, 0)
+            lines.append(f"    const int32_t inv{k} = {c};")
+        lines.append("    if (!(" + " | ".join(f"(inv{k} != 0)" for k in range(len(invs))) + f")) fb |= 1u << {slot};")
+        slot += 1
+        for k in range(len(invs)):
+            lines.append(f"    if (inv{k} == 0) fb |= 1u << {slot};")
+            slot += 1
+    term = None
+    for name, f in spec.properties:
+        if name == "Termination":
+            term, _ = gen.gen(f, False, 0)
+            continue
+        c, _ = gen.gen(f, False, 0)
+        lines.append(f"    if (({c}) == 0) fb |= 1u << {slot};  // {name}")
+        slot += 1
+    if spec.safety_predicate is not None:
+        c, _ = gen.gen(spec.safety_predicate, False, 0)
+        lines.append(f"    if (({c}) == 0) fb |= 1u << {slot};  // SafetyPredicate")
+        slot += 1
+    assert slot == len(prog.slot_entry)
+    if gen.max_vi > 4:
+        raise FormulaError("more than 4 nested V.exists over Int")
+    rel = sum(1 << s for s, fl in enumerate(prog.slot_flags) if fl & SPEC_RELATIONAL)
+    fmask = sum(1 << f for f in gen.fields)
+    tmask = sum(1 << t for t in gen.tags)
+    src = [
+        "// generated by round_amd/formula.py (codegen_hip): native checker of one Spec",
+        '#include "psg_spec_native.hpp"',
+        "namespace psg {",
+        "struct GenSpec {",
+        f"  static constexpr int kSlots = {slot};",
+        f"  static constexpr uint32_t kRelational = {rel}u;",
+        f"  static constexpr bool kHasTerm = {'true' if term else 'false'};",
+        f"  static constexpr uint32_t kFields = {fmask}u;",
+        f"  static constexpr uint32_t kTags = {tmask}u;",
+        "  template <int W>",
+        "  __device__ static uint32_t fail(spec::Ctx<W>& x, int32_t* scratch) {",
+        "    (void)scratch;",
+        "    uint32_t fb = 0;",
+        *lines,
+        "    return fb;",
+        "  }",
+        "  template <int W>",
+        "  __device__ static bool term(spec::Ctx<W>& x, int32_t* scratch) {",
+        "    (void)scratch;",
+        f"    return ({term or '0'}) != 0;",
+        "  }",
+        "};",
+        "}  // namespace psg",
+        "PSG_SPEC_NATIVE_KERNELS(psg::GenSpec)",
+        "",
+    ]
+    return "\n".join(src), prog
+
+
+def compile_native(spec: Spec, alg: Optional[int] = None, cache_dir: str = None, hipcc: str = None) -> Program:
+    """Lower `spec` to native gfx950 code (hipcc --genco, cached by source hash) and
+    return a Program whose module_path psg_run_batch_spec launches instead of the
+    bytecode interpreter."""
+    import hashlib
+    import os
+    import subprocess
+    src, prog = codegen_hip(spec, alg)
+    cache_dir = cache_dir or CACHE_DIR
+    os.makedirs(cache_dir, exist_ok=True)
+    hdrs = "".join(open(os.path.join(_CSRC, h)).read() for h in ("psg_spec_native.hpp", "psg_device.hpp"))
+    key = hashlib.sha256((src + hdrs + open(os.path.join(_INCLUDE, "psg.h")).read()).encode()).hexdigest()[:24]
+    out = os.path.join(cache_dir, f"spec_{key}.co")
+    if not os.path.exists(out):
+        path = os.path.join(cache_dir, f"spec_{key}.hip")
+        with open(path, "w") as f:
+            f.write(src)
+        cmd = [hipcc or os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), "--genco", "--offload-arch=gfx950", "-O3",
+               "-std=c++17", "-I", _CSRC, "-I", _INCLUDE, path, "-o", out + ".tmp"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise FormulaError("native spec compile failed:\n" + r.stderr[-4000:])
+        os.replace(out + ".tmp", out)
+    prog.module_path = out
+    return prog

@@ -1,9 +1,10 @@
 """GPU: compiled Spec programs (psg_run_batch_spec, psg_spec_vm.hip).
 
-1. The reference Specs compiled from the Python DSL and evaluated by the device
-   interpreter give exactly the per-instance results of the hand-lowered
-   kernels (same run: digests, first failing check point per slot, termination).
-2. Custom specs: device interpreter over the device trace == CPU interpreter over
+1. The reference Specs compiled from the Python DSL and evaluated on the device —
+   by the bytecode interpreter and as native lowered wave code (compile_native) —
+   give exactly the per-instance results of the hand-lowered kernels (same run:
+   digests, first failing check point per slot, termination).
+2. Custom specs: both device paths over the device trace == CPU interpreter over
    the oracle trace, bit for bit, incl. n > 64 (lane quantifiers in 64-pid passes).
 """
 import pytest
@@ -33,9 +34,14 @@ def _rows(pi, k):
     return [(tuple(s.first_fail)[:k], s.term_round) for s in pi]
 
 
+def _prog(spec, alg_id, mode):
+    return F.compile_native(spec, alg_id) if mode == "native" else F.compile_spec(spec, alg_id)
+
+
+@pytest.mark.parametrize("mode", ["vm", "native"])
 @pytest.mark.parametrize("cid,alg,n,count,kw", REF, ids=[c[0] for c in REF])
-def test_reference_spec_program_matches_builtin_checks(cid, alg, n, count, kw):
-    prog = F.compile_spec(F.REFERENCE_SPECS[alg.alg_id](), alg.alg_id)
+def test_reference_spec_program_matches_builtin_checks(cid, alg, n, count, kw, mode):
+    prog = _prog(F.REFERENCE_SPECS[alg.alg_id](), alg.alg_id, mode)
     k = len(prog.slot_names)
     with psync.GpuRound(alg, n, batch_capacity=count, **kw) as gr:
         built = gr.run(0, count, per_instance=True)
@@ -46,9 +52,10 @@ def test_reference_spec_program_matches_builtin_checks(cid, alg, n, count, kw):
     assert spec.summary.digest == built.summary.digest
 
 
+@pytest.mark.parametrize("mode", ["vm", "native"])
 @pytest.mark.parametrize("cid,alg,n,kw,mk", spec_cases.CUSTOM, ids=[c[0] for c in spec_cases.CUSTOM])
-def test_custom_spec_matches_cpu_interpreter(cid, alg, n, kw, mk, oracle_mod):
-    prog = F.compile_spec(mk(), alg.alg_id)
+def test_custom_spec_matches_cpu_interpreter(cid, alg, n, kw, mk, oracle_mod, mode):
+    prog = _prog(mk(), alg.alg_id, mode)
     count = 300 if n <= 16 else 60
     with psync.GpuRound(alg, n, batch_capacity=count, seed=19, **kw) as gr:
         res = gr.run_spec(100, count, prog, per_instance=True)
