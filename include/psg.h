@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PSG_ABI_VERSION 2u
+#define PSG_ABI_VERSION 3u
 
 /* Algorithms, keyed on the reference class names. */
 enum psg_alg {
@@ -258,8 +258,10 @@ int psg_run_batch(psg_ctx* ctx, uint64_t inst_begin, uint64_t inst_count,
  * int32 and decision_round [count][n] int32 (-1 = none). Either may be NULL. */
 int psg_copy_decisions(psg_ctx* ctx, int32_t* decision, int32_t* decision_round);
 
-/* Re-execute the listed global instance ids (seeded inputs) and return their
- * summaries (k entries) and per-process records (k * n entries, nullable). */
+/* Re-execute the listed global instance ids and return their summaries (k
+ * entries) and per-process records (k * n entries, nullable). Inputs: the staged
+ * ones (psg_load_inputs) when every id lies in the staged range, else seeded;
+ * HO sets: the loaded explicit schedule (every id must lie in its range) or seeded. */
 int psg_fetch_instances(psg_ctx* ctx, const uint64_t* ids, size_t k,
                         psg_instance_summary* sums, psg_process_record* procs);
 
@@ -281,6 +283,37 @@ int psg_copy_decisions_f64(psg_ctx* ctx, double* decision, int32_t* decision_rou
 /* psg_fetch_instances plus the Double decision and final x of each process ([k][n] each, nullable). */
 int psg_fetch_instances_f64(psg_ctx* ctx, const uint64_t* ids, size_t k, psg_instance_summary* sums,
                             psg_process_record* procs, double* decision, double* final_x);
+
+/* ---------------------------------------------------------------------------
+ * Explicit HO schedules (replayable counterexamples and the
+ * adversary search; the in-JVM harness of §8c driven by identical HO sets).
+ *
+ * In the reference an HO set is whatever the network delivered before the
+ * round's timeout (psync/Round.scala:57-69, psync/runtime/InstanceHandler.scala:
+ * 164-258); `Process.HO` is its Spec-level name (psync/Process.scala:14). Here it
+ * is data: ho[inst][k][p] = HO(p) in round k as W = ceil(n/64) little-endian
+ * 64-bit words (bit q of word w = process 64w+q), layout [count][R][n][W] uint64.
+ * Sets are used verbatim (no self bit, no ho_min, no good rounds; bits >= n are
+ * ignored). crash_round [count][n] (nullable: every process correct) only marks
+ * processes as crashed for the checks that quantify over correct processes
+ * (FloodMin / KSet k-agreement); the omissions themselves are in the HO sets.
+ * ------------------------------------------------------------------------- */
+
+/* Stage an explicit schedule for instances [inst_begin, inst_begin+inst_count)
+ * (count <= batch_capacity). Until psg_clear_schedule, psg_run_batch,
+ * psg_run_batch_spec and psg_fetch_instances read HO sets from it and accept only
+ * instances inside its range (PSG_ERANGE otherwise). Initial values still come
+ * from psg_load_inputs (or are seeded); BenOr coins stay seeded by instance id. */
+int psg_load_schedule(psg_ctx* ctx, uint64_t inst_begin, uint64_t inst_count, const uint64_t* ho,
+                      const int32_t* crash_round);
+/* Return to seeded HO schedules. */
+int psg_clear_schedule(psg_ctx* ctx);
+/* Export the seeded schedule of instances [inst_begin, inst_begin+inst_count)
+ * in the explicit layout: ho [count][R][n][W] and crash_round [count][n] (-1 =
+ * correct; nullable). Replaying it with psg_load_schedule reproduces the seeded
+ * run bit for bit. Any count (processed in device chunks). */
+int psg_materialize_schedule(psg_ctx* ctx, uint64_t inst_begin, uint64_t inst_count, uint64_t* ho,
+                             int32_t* crash_round);
 
 const char* psg_last_error(const psg_ctx* ctx);
 void psg_destroy(psg_ctx* ctx);

@@ -71,6 +71,14 @@ def lib():
         L.oracle_init_value.restype = C.c_int32
         L.oracle_crash_round.argtypes = [C.POINTER(abi.Config), C.c_uint64, C.c_int32]
         L.oracle_crash_round.restype = C.c_int32
+        L.oracle_run_schedule.argtypes = [C.POINTER(abi.Config), C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_void_p, C.POINTER(abi.Summary),
+                                          C.POINTER(abi.InstanceSummary), C.POINTER(abi.ProcessRecord),
+                                          C.c_void_p, C.c_void_p, C.c_int32]
+        L.oracle_run_schedule.restype = C.c_int
+        L.oracle_materialize_schedule.argtypes = [C.POINTER(abi.Config), C.c_uint64, C.c_uint64, C.c_void_p,
+                                                  C.c_void_p]
+        L.oracle_materialize_schedule.restype = C.c_int
         _lib = L
     return _lib
 
@@ -236,3 +244,46 @@ def vm_run(program, tr, count, n, rounds):
     _check(lib().oracle_vm_run(C.byref(cp), tr, count, n, rounds, ff, tm))
     k = len(program.slot_entry)
     return [list(ff[i * abi.PSG_MAX_CHECKS:i * abi.PSG_MAX_CHECKS + k]) for i in range(count)], list(tm)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def run_schedule(cfg, inst_begin, count, ho, crash=None, init=None, per_instance=False, records=False,
+                 threads=8):
+    """Instances under an explicit schedule (psg_load_schedule semantics).
+
+    ho: uint64 [count][R][n][W]; crash: int32 [count][n] or None; init: [count][n]
+    int32 (Doubles for EpsilonConsensus) or None = seeded. Returns (Summary,
+    [InstanceSummary], [ProcessRecord], decisions, final_x) — the last two only for
+    real-valued algorithms with records=True."""
+    import numpy as np
+    real = cfg.alg == abi.PSG_ALG_EPSILON
+    W = (cfg.n + 63) // 64
+    ho = np.ascontiguousarray(ho, dtype=np.uint64).reshape(count, cfg.rounds, cfg.n, W)
+    cr = None if crash is None else np.ascontiguousarray(crash, dtype=np.int32).reshape(count, cfg.n)
+    ini = None
+    if init is not None:
+        ini = np.ascontiguousarray(init, dtype=np.float64 if real else np.int32).reshape(count, cfg.n)
+    summ = abi.Summary()
+    pi = (abi.InstanceSummary * count)() if per_instance else None
+    cells = count * cfg.n
+    rec = (abi.ProcessRecord * cells)() if records else None
+    dec = np.zeros(cells, np.float64) if (records and real) else None
+    fx = np.zeros(cells, np.float64) if (records and real) else None
+    rc = lib().oracle_run_schedule(C.byref(cfg), inst_begin, count, None if real else _ptr(ini),
+                                   _ptr(ini) if real else None, _ptr(ho), _ptr(cr), C.byref(summ), pi, rec,
+                                   _ptr(dec), _ptr(fx), threads)
+    _check(rc)
+    return (summ, (list(pi) if pi is not None else None), (list(rec) if rec is not None else None), dec, fx)
+
+
+def materialize_schedule(cfg, inst_begin, count):
+    """The seeded schedule in the explicit layout: (ho uint64 [count][R][n][W], crash int32 [count][n])."""
+    import numpy as np
+    W = (cfg.n + 63) // 64
+    ho = np.zeros((count, cfg.rounds, cfg.n, W), np.uint64)
+    cr = np.zeros((count, cfg.n), np.int32)
+    _check(lib().oracle_materialize_schedule(C.byref(cfg), inst_begin, count, _ptr(ho), _ptr(cr)))
+    return ho, cr

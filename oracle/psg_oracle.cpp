@@ -1291,8 +1291,16 @@ struct InstOut {
   std::string msg;
 };
 
-struct ExplicitHO { /* test hook: explicit HO masks [R][n] (n <= 64), explicit crash info */
+/* Explicit HO schedule of one instance (psg_load_schedule semantics, psg.h):
+ * ho[(k * n + p) * W + w] = word w of HO(p) in round k, used verbatim (bits >= n
+ * ignored). crash (nullable) = crash round per process for the never-crashed
+ * classification; `legacy` keeps the single-instance KAT hook's behaviour
+ * (crash classification from the seeded draw). */
+struct ExplicitHO {
   const uint64_t* ho = nullptr;
+  int W = 1;
+  const int32_t* crash = nullptr;
+  bool legacy = true;
 };
 
 template <class Alg>
@@ -1342,7 +1350,8 @@ static void run_engine(Alg& alg, const psg_config& cfg, uint64_t inst, const int
   };
   snapshot(finit);
   std::vector<bool> crashed(n);
-  for (int p = 0; p < n; ++p) crashed[p] = sch.crashed(p);
+  for (int p = 0; p < n; ++p)
+    crashed[p] = (eho && !eho->legacy) ? (eho->crash != nullptr && eho->crash[p] >= 0) : sch.crashed(p);
 
   const int nck = n_checks_of(cfg.alg);
   psg_instance_summary& S = out.sum;
@@ -1399,8 +1408,8 @@ static void run_engine(Alg& alg, const psg_config& cfg, uint64_t inst, const int
       if (halted[p]) continue;
       Bits ho;
       if (eho && eho->ho) {
-        uint64_t m = eho->ho[(size_t)k * n + p];
-        for (int q = 0; q < n; ++q) if ((m >> q) & 1) ho.set(q);
+        const uint64_t* m = eho->ho + ((size_t)k * n + p) * (size_t)eho->W;
+        for (int q = 0; q < n; ++q) if ((m[q >> 6] >> (q & 63)) & 1) ho.set(q);
       } else {
         ho = sch.ho(k, p);
       }
@@ -1644,7 +1653,8 @@ int32_t oracle_crash_round(const psg_config* cfg, uint64_t inst, int32_t p) {
  * any disagreement). */
 static int run_impl(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const uint64_t* ids,
                     const int32_t* init, const double* init_real, psg_summary* out, psg_instance_summary* per_inst,
-                    psg_process_record* recs, double* fdec, double* fx, int32_t threads, int32_t spec_mode);
+                    psg_process_record* recs, double* fdec, double* fx, int32_t threads, int32_t spec_mode,
+                    const uint64_t* sched_ho = nullptr, const int32_t* sched_crash = nullptr);
 
 int oracle_run(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const uint64_t* ids,
                const int32_t* init, psg_summary* out, psg_instance_summary* per_inst,
@@ -1663,7 +1673,8 @@ int oracle_run_real(const psg_config* cfg, uint64_t inst_begin, uint64_t count, 
 
 static int run_impl(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const uint64_t* ids,
                     const int32_t* init, const double* init_real, psg_summary* out, psg_instance_summary* per_inst,
-                    psg_process_record* recs, double* fdec, double* fx, int32_t threads, int32_t spec_mode) {
+                    psg_process_record* recs, double* fdec, double* fx, int32_t threads, int32_t spec_mode,
+                    const uint64_t* sched_ho, const int32_t* sched_crash) {
   std::string err;
   int rc = orc::validate(cfg, err);
   if (rc) { g_oracle_err = err; return rc; }
@@ -1679,7 +1690,15 @@ static int run_impl(const psg_config* cfg, uint64_t inst_begin, uint64_t count, 
     for (uint64_t i = lo; i < hi; ++i) {
       uint64_t inst = ids ? ids[i] : inst_begin + i;
       orc::InstOut o;
-      orc::run_one(*cfg, inst, init ? init + i * (uint64_t)n : nullptr, spec_mode, nullptr, o, false,
+      orc::ExplicitHO e;
+      if (sched_ho) {
+        const int W = (n + 63) / 64;
+        e.ho = sched_ho + i * (uint64_t)R * (uint64_t)n * (uint64_t)W;
+        e.W = W;
+        e.crash = sched_crash ? sched_crash + i * (uint64_t)n : nullptr;
+        e.legacy = false;
+      }
+      orc::run_one(*cfg, inst, init ? init + i * (uint64_t)n : nullptr, spec_mode, sched_ho ? &e : nullptr, o, false,
                    init_real ? init_real + i * (uint64_t)n : nullptr);
       if (o.mismatch) { bad = 1; errs[t] = o.msg; }
       s.instances += 1;
@@ -1799,6 +1818,40 @@ int oracle_run_explicit(const psg_config* cfg, const int32_t* init, const uint64
   if (recs) std::memcpy(recs, o.rec.data(), sizeof(psg_process_record) * cfg->n);
   if (trace) std::memcpy(trace, o.trace.data(), sizeof(int64_t) * o.trace.size());
   if (o.mismatch) { g_oracle_err = o.msg; return PSG_EIO; }
+  return 0;
+}
+
+/* Instances [inst_begin, inst_begin+count) under an explicit schedule
+ * ho [count][R][n][W] (crash [count][n] nullable), psg_load_schedule semantics.
+ * init: [count][n] int32 (nullable = seeded); init_real likewise for Doubles. */
+int oracle_run_schedule(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const int32_t* init,
+                        const double* init_real, const uint64_t* ho, const int32_t* crash, psg_summary* out,
+                        psg_instance_summary* per_inst, psg_process_record* recs, double* fdec, double* fx,
+                        int32_t threads) {
+  if (!ho && count) { g_oracle_err = "null schedule"; return PSG_EINVAL; }
+  return run_impl(cfg, inst_begin, count, nullptr, init, init_real, out, per_inst, recs, fdec, fx, threads, 0, ho,
+                  crash);
+}
+
+/* The seeded schedule of instances [inst_begin, inst_begin+count) in the explicit
+ * layout (psg_materialize_schedule): ho [count][R][n][W], crash [count][n] (nullable). */
+int oracle_materialize_schedule(const psg_config* cfg, uint64_t inst_begin, uint64_t count, uint64_t* ho,
+                                int32_t* crash) {
+  std::string err;
+  int rc = orc::validate(cfg, err);
+  if (rc) { g_oracle_err = err; return rc; }
+  const int n = cfg->n, R = cfg->rounds, W = (n + 63) / 64;
+  for (uint64_t i = 0; i < count; ++i) {
+    orc::Schedule s(*cfg, inst_begin + i);
+    if (crash) for (int p = 0; p < n; ++p) crash[i * (uint64_t)n + p] = s.crash_round[p];
+    for (int k = 0; k < R; ++k)
+      for (int p = 0; p < n; ++p) {
+        orc::Bits b = s.ho(k, p);
+        uint64_t* q = ho + ((i * (uint64_t)R + (uint64_t)k) * (uint64_t)n + (uint64_t)p) * (uint64_t)W;
+        for (int w = 0; w < W; ++w) q[w] = 0;
+        for (int x = 0; x < n; ++x) if (b.test(x)) q[x >> 6] |= 1ULL << (x & 63);
+      }
+  }
   return 0;
 }
 

@@ -5,7 +5,7 @@ binding (oracle/oracle.py): both libraries speak the same C structs.
 """
 import ctypes as C
 
-PSG_ABI_VERSION = 2
+PSG_ABI_VERSION = 3
 
 PSG_ALG_OTR = 1
 PSG_ALG_LAST_VOTING = 2

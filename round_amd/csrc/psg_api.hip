@@ -66,6 +66,12 @@ struct psg_ctx {
   hipFunction_t native_fn = nullptr;
   bool staged = false;
   uint64_t staged_begin = 0, staged_count = 0;
+  // explicit schedule (psg_load_schedule)
+  uint64_t* d_ho = nullptr;
+  int32_t* d_crash = nullptr;
+  uint64_t ho_cap = 0;  // instances d_ho / d_crash hold
+  bool ho_loaded = false, ho_has_crash = false;
+  uint64_t ho_begin = 0, ho_count = 0;
   int32_t* d_dec = nullptr;
   uint8_t* d_dround = nullptr;
   psg_instance_summary* d_inst = nullptr;
@@ -169,7 +175,20 @@ static KArgs make_args(const psg_ctx* c) {
   a.ho_min = f.sched.ho_min;
   a.self_bit = f.sched.self_bit;
   a.counters = c->d_counters;
+  if (c->ho_loaded) {
+    a.ho_in = c->d_ho;
+    a.crash_in = c->ho_has_crash ? c->d_crash : nullptr;
+    a.ho_base = c->ho_begin;
+  }
   return a;
+}
+
+// Instances [begin, begin+count) must lie inside a loaded explicit schedule.
+static int check_sched_range(psg_ctx* c, uint64_t begin, uint64_t count) {
+  if (!c->ho_loaded || count == 0) return PSG_OK;
+  if (begin < c->ho_begin || begin - c->ho_begin > c->ho_count || count > c->ho_count - (begin - c->ho_begin))
+    return fail(c, PSG_ERANGE, "instances outside the loaded explicit schedule");
+  return PSG_OK;
 }
 
 static int groups_per_block(int W) { return W == 1 ? 4 : 1; }
@@ -461,6 +480,7 @@ int psg_run_batch(psg_ctx* c, uint64_t inst_begin, uint64_t count, psg_summary* 
     return PSG_OK;
   }
   if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  if (int rc = check_sched_range(c, inst_begin, count)) return rc;
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (!(c->staged && c->staged_begin == inst_begin && c->staged_count == count)) {
     int rc = psg_load_inputs(c, inst_begin, count, nullptr);
@@ -550,6 +570,7 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
   std::string m;
   if (validate_prog(prog, m)) return fail(c, PSG_EINVAL, m);
   if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  if (int rc = check_sched_range(c, inst_begin, count)) return rc;
   if (out) std::memset(out, 0, sizeof(*out));
   if (count == 0) return PSG_OK;
   HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -714,12 +735,23 @@ static int fetch_impl(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_su
     }
     c->fetch_cap = k;
   }
+  bool in_staged = c->staged;
+  for (size_t j = 0; j < k; ++j) {
+    if (int rc = check_sched_range(c, ids[j], 1)) return rc;
+    if (ids[j] < c->staged_begin || ids[j] - c->staged_begin >= c->staged_count) in_staged = false;
+  }
   HIPCHK(c, hipMemcpyAsync(c->d_ids, ids, sizeof(uint64_t) * k, hipMemcpyHostToDevice, c->stream));
   KArgs a = make_args(c);
   a.inst_begin = 0;
   a.count = k;
   a.ids = c->d_ids;
-  a.init = nullptr;  // seeded inputs of each listed id
+  // inputs of each listed id: the staged rows when all ids are staged, else seeded
+  a.init = nullptr;
+  if (in_staged) {
+    a.init_base = c->staged_begin;
+    if (c->cfg.alg == PSG_ALG_EPSILON) a.init_f64 = c->init_f64_host ? c->d_init_f64 : nullptr;
+    else a.init = c->d_init;
+  }
   a.out_inst = c->d_inst;
   a.out_rec = c->d_rec;
   a.out_rec_f64 = c->d_rec_f64;
@@ -743,6 +775,80 @@ static int fetch_impl(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_su
   return PSG_OK;
 }
 
+int psg_load_schedule(psg_ctx* c, uint64_t inst_begin, uint64_t count, const uint64_t* ho,
+                      const int32_t* crash_round) {
+  if (!c) return PSG_EINVAL;
+  if (!ho && count) return fail(c, PSG_EINVAL, "null schedule");
+  if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const uint64_t n = (uint64_t)c->cfg.n, R = (uint64_t)c->cfg.rounds, W = (uint64_t)c->W;
+  if (count > c->ho_cap) {
+    if (c->d_ho) (void)hipFree(c->d_ho);
+    if (c->d_crash) (void)hipFree(c->d_crash);
+    c->d_ho = nullptr;
+    c->d_crash = nullptr;
+    c->ho_cap = 0;
+    c->ho_loaded = false;
+    HIPCHK(c, hipMalloc(&c->d_ho, sizeof(uint64_t) * count * R * n * W));
+    HIPCHK(c, hipMalloc(&c->d_crash, sizeof(int32_t) * count * n));
+    c->ho_cap = count;
+  }
+  if (count) {
+    HIPCHK(c, hipMemcpyAsync(c->d_ho, ho, sizeof(uint64_t) * count * R * n * W, hipMemcpyHostToDevice, c->stream));
+    if (crash_round)
+      HIPCHK(c, hipMemcpyAsync(c->d_crash, crash_round, sizeof(int32_t) * count * n, hipMemcpyHostToDevice,
+                               c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  c->ho_loaded = true;
+  c->ho_has_crash = crash_round != nullptr;
+  c->ho_begin = inst_begin;
+  c->ho_count = count;
+  return PSG_OK;
+}
+
+int psg_clear_schedule(psg_ctx* c) {
+  if (!c) return PSG_EINVAL;
+  c->ho_loaded = false;
+  c->ho_has_crash = false;
+  c->ho_begin = c->ho_count = 0;
+  return PSG_OK;
+}
+
+int psg_materialize_schedule(psg_ctx* c, uint64_t inst_begin, uint64_t count, uint64_t* ho, int32_t* crash_round) {
+  if (!c) return PSG_EINVAL;
+  if (!ho && count) return fail(c, PSG_EINVAL, "null output");
+  if (count == 0) return PSG_OK;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const uint64_t n = (uint64_t)c->cfg.n, R = (uint64_t)c->cfg.rounds, W = (uint64_t)c->W;
+  const uint64_t per = R * n * W * sizeof(uint64_t);
+  const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(count, (256ull << 20) / per));
+  uint64_t* d_out = nullptr;
+  int32_t* d_cr = nullptr;
+  hipError_t e = hipMalloc(&d_out, per * chunk);
+  if (e == hipSuccess) e = hipMalloc(&d_cr, sizeof(int32_t) * n * chunk);
+  int rc = PSG_OK;
+  KArgs a = make_args(c);
+  a.ho_in = nullptr;  // always the seeded generator
+  a.crash_in = nullptr;
+  const int G = groups_per_block(c->W);
+  for (uint64_t off = 0; e == hipSuccess && off < count; off += chunk) {
+    const uint64_t m = std::min<uint64_t>(chunk, count - off);
+    a.inst_begin = inst_begin + off;
+    a.count = m;
+    const int grid = (int)std::min<uint64_t>((m + G - 1) / G, (uint64_t)c->grid_max);
+    e = launch_schedule(a, c->W, grid, d_out, d_cr, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(ho + off * R * n * W, d_out, per * m, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && crash_round)
+      e = hipMemcpyAsync(crash_round + off * n, d_cr, sizeof(int32_t) * n * m, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  }
+  if (e != hipSuccess) rc = hip_fail(c, e, "psg_materialize_schedule");
+  if (d_out) (void)hipFree(d_out);
+  if (d_cr) (void)hipFree(d_cr);
+  return rc;
+}
+
 const char* psg_last_error(const psg_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
 
 void psg_destroy(psg_ctx* c) {
@@ -763,6 +869,8 @@ void psg_destroy(psg_ctx* c) {
   if (c->d_vm_counters) (void)hipFree(c->d_vm_counters);
   if (c->d_vm_err) (void)hipFree(c->d_vm_err);
   if (c->d_prog) (void)hipFree(c->d_prog);
+  if (c->d_ho) (void)hipFree(c->d_ho);
+  if (c->d_crash) (void)hipFree(c->d_crash);
   if (c->module) (void)hipModuleUnload(c->module);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);

@@ -39,7 +39,7 @@ PSG_DEV void benor_check(Grp<W>& g, Checks& ck, int c, bool has_old, int n, cons
   ck.record(fb, meq(D, full), c, g.lane);
 }
 
-template <int W>
+template <int W, bool XHO>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[2 * W];
@@ -49,18 +49,18 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
   Grp<W> g;
   grp_setup(g, a, xb, red);
   constexpr int G = Geometry<W>::kGroups;
-  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int grp = W == 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
   const int n = a.n;
   const int thr = a.variant == 1 ? n / 4 : n / 2;  // BenOr.scala:68, 71 (variant 1: mutation)
   const Mask<W> full = mfull<W>(n);
 
   for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
-    Sched<W> sc;
+    Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
     sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
-    if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_BENOR);
+    if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_BENOR);
     // BenOrProcess state after init(io) (BenOr.scala:13-28); vote starts as None
     bool x = x0 != 0, cd = false, decided = false, decision = false, halted = false;
     int vote = -1;  // Option[Boolean]: -1 None, 0 Some(false), 1 Some(true)
@@ -147,7 +147,8 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
 
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(benor_kernel<W>, dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  if (a.ho_in) hipLaunchKernelGGL((benor_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  else hipLaunchKernelGGL((benor_kernel<W, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -163,10 +164,10 @@ hipError_t launch_benor(const KArgs& a, int W, int grid, hipStream_t s) {
 
 const void* benor_kernel_ptr(int W) {
   switch (W) {
-    case 1: return (const void*)benor_kernel<1>;
-    case 2: return (const void*)benor_kernel<2>;
-    case 3: return (const void*)benor_kernel<3>;
-    case 4: return (const void*)benor_kernel<4>;
+    case 1: return (const void*)benor_kernel<1, false>;
+    case 2: return (const void*)benor_kernel<2, false>;
+    case 3: return (const void*)benor_kernel<3, false>;
+    case 4: return (const void*)benor_kernel<4, false>;
   }
   return nullptr;
 }

@@ -38,7 +38,18 @@ struct KArgs {
   uint32_t drop_log2, good_p32;
   int32_t good_min, crash_fmax, ho_min;
   uint32_t self_bit;
+  // explicit schedule (psg_load_schedule): HO(p, k) of global instance id `inst` is
+  // ho_in[((inst - ho_base) * R + k) * n + p][0..W-1]; crash_in[(inst - ho_base) * n + p]
+  // (nullable) = crash round for the never-crashed classification, -1 = correct
+  const uint64_t* ho_in;
+  const int32_t* crash_in;
+  uint64_t ho_base;
+  uint64_t init_base;  // fetch path with staged inputs: init row of id `inst` is inst - init_base
 };
+
+// Initial value of process pid of batch element i (global id inst): staged rows
+// are indexed by batch position, or by global id in the fetch (ids) path.
+PSG_DEV uint64_t init_row(const KArgs& a, uint64_t i, uint64_t inst) { return a.ids ? inst - a.init_base : i; }
 
 // Spec-program interpreter arguments (psg_spec_vm.hip)
 struct VmArgs {
@@ -494,7 +505,9 @@ PSG_DEV void lds_sync() {
 }
 
 // ---------------------------------------------------------------- schedule
-template <int W>
+// XHO: explicit schedule (psg_load_schedule) — HO sets read from HBM instead of
+// drawn; a separate instantiation so the seeded hot path keeps its registers.
+template <int W, bool XHO = false>
 struct Sched {
   uint64_t seed, inst;
   Mask<W> full;
@@ -502,8 +515,28 @@ struct Sched {
   bool crash_on;
   int good_min, ho_min, V;
   uint32_t drop, good_p32, self_bit;
+  int nproc;
+  const uint64_t* hop;  // explicit schedule of this instance ([R][n][W] words), or null
 
   PSG_DEV void setup(const KArgs& args, uint64_t i, int pid, bool valid) {
+    hop = nullptr;
+    nproc = args.n;
+    if constexpr (XHO) {  // explicit schedule: HO sets read verbatim, no seeded draws
+      const uint64_t row = i - args.ho_base;
+      hop = args.ho_in + row * (uint64_t)args.R * (uint64_t)args.n * W;
+      seed = args.seed;
+      inst = i;
+      V = args.V;
+      drop = 0;
+      good_p32 = 0;
+      self_bit = 0;
+      ho_min = -1;
+      full = mfull<W>(args.n);
+      crash_on = false;
+      good_min = 0;
+      crash_round = (args.crash_in && valid) ? args.crash_in[row * (uint64_t)args.n + pid] : -1;
+      return;
+    }
     seed = args.seed;
     inst = i;
     V = args.V;
@@ -584,6 +617,15 @@ struct Sched {
   // word cache): word j < W*drop feeds drop mask j / drop, word W*drop + w is
   // the crash-round survival mask of word w.
   PSG_DEV Mask<W> ho(int k, int pid, bool good, const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CN) const {
+    if constexpr (XHO) {  // explicit: W contiguous words per process, the wave reads 512*W contiguous bytes
+      Mask<W> m = mzero<W>();
+      if (pid < nproc) {
+        const uint64_t* q = hop + ((uint64_t)k * (uint64_t)nproc + (uint64_t)pid) * W;
+#pragma unroll
+        for (int w = 0; w < W; ++w) m.w[w] = __builtin_nontemporal_load(q + w) & full.w[w];
+      }
+      return m;
+    }
     const uint32_t nd = (uint32_t)W * drop;
     const uint32_t j0 = good ? nd : 0u;
     const uint32_t j1 = crash_on ? nd + (uint32_t)W : (good ? 0u : nd);

@@ -65,7 +65,7 @@ PSG_DEV void eps_check(Grp<W>& g, Checks& ck, int c, const Mask<W>& full, bool d
   ck.record(fbit(agree, 0) | fbit(valid, 1) | fbit(pred, 2), meq(g.ballot(decided), full), c, g.lane);
 }
 
-template <int W>
+template <int W, bool XHO>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[2 * W];
@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a)
   Grp<W> g;
   grp_setup(g, a, xb, red);
   constexpr int G = Geometry<W>::kGroups;
-  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int grp = W == 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
   const int n = a.n;
   const int f = a.param;
   const double eps = a.real_param;
@@ -87,13 +87,13 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a)
 
   for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
-    Sched<W> sc;
+    Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
     sc.prep_good(0, g.lane, a.R);
     double x0 = 0.0;
     if (g.valid) {
       if (a.init_f64) {
-        x0 = a.init_f64[i * (uint64_t)n + g.pid];
+        x0 = a.init_f64[init_row(a, i, inst) * (uint64_t)n + g.pid];
       } else {  // uniform [0,1) with 53 bits (Random.nextDouble shape, Epsilon.scala:94)
         const uint64_t w = rword(a.seed, inst, ROUND_INIT, (uint32_t)g.pid, 0);
         x0 = (double)(w >> 11) * 0x1.0p-53;
@@ -202,7 +202,8 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a)
 
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(epsilon_kernel<W>, dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  if (a.ho_in) hipLaunchKernelGGL((epsilon_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  else hipLaunchKernelGGL((epsilon_kernel<W, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -218,10 +219,10 @@ hipError_t launch_epsilon(const KArgs& a, int W, int grid, hipStream_t s) {
 
 const void* epsilon_kernel_ptr(int W) {
   switch (W) {
-    case 1: return (const void*)epsilon_kernel<1>;
-    case 2: return (const void*)epsilon_kernel<2>;
-    case 3: return (const void*)epsilon_kernel<3>;
-    case 4: return (const void*)epsilon_kernel<4>;
+    case 1: return (const void*)epsilon_kernel<1, false>;
+    case 2: return (const void*)epsilon_kernel<2, false>;
+    case 3: return (const void*)epsilon_kernel<3, false>;
+    case 4: return (const void*)epsilon_kernel<4, false>;
   }
   return nullptr;
 }

@@ -45,7 +45,7 @@ PSG_DEV Mask<W> load_t(const uint64_t* ts, int q) {
   return m;
 }
 
-template <int W>
+template <int W, bool XHO>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[2 * W];
@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
   Grp<W> g;
   grp_setup(g, a, xb, red);
   constexpr int G = Geometry<W>::kGroups;
-  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int grp = W == 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
   const int n = a.n;
   const int kk = a.param;
   const int need = a.variant == 1 ? 1 : n - kk;  // same.size > n - k (KSetAgreement.scala:56)
@@ -68,12 +68,12 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
 
   for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
-    Sched<W> sc;
+    Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
     sc.prep_good(0, g.lane, a.R);
     const bool crashed = sc.crash_round >= 0;
     int32_t x0 = 0;
-    if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_KSET);
+    if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_KSET);
     x0s[g.pid] = x0;
     X0Set<W> X0;
     X0.build(g, x0tab[grp], x0);
@@ -213,7 +213,8 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
 
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(kset_kernel<W>, dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  if (a.ho_in) hipLaunchKernelGGL((kset_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  else hipLaunchKernelGGL((kset_kernel<W, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -229,10 +230,10 @@ hipError_t launch_kset(const KArgs& a, int W, int grid, hipStream_t s) {
 
 const void* kset_kernel_ptr(int W) {
   switch (W) {
-    case 1: return (const void*)kset_kernel<1>;
-    case 2: return (const void*)kset_kernel<2>;
-    case 3: return (const void*)kset_kernel<3>;
-    case 4: return (const void*)kset_kernel<4>;
+    case 1: return (const void*)kset_kernel<1, false>;
+    case 2: return (const void*)kset_kernel<2, false>;
+    case 3: return (const void*)kset_kernel<3, false>;
+    case 4: return (const void*)kset_kernel<4, false>;
   }
   return nullptr;
 }

@@ -66,7 +66,7 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
   ck.record(fb, term, c, g.lane);
 }
 
-template <int W, bool V2>
+template <int W, bool V2, bool XHO>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[2 * W];
@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
   Grp<W> g;
   grp_setup(g, a, xb, red);
   constexpr int G = Geometry<W>::kGroups;
-  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
+  const int grp = W == 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
   const int n = a.n;
   const int thr = a.variant == 1 ? n / 2 : (2 * n) / 3;  // Otr.scala:64, 67 (variant 1: mutation)
   const Mask<W> full = mfull<W>(n);
@@ -86,11 +86,11 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
 
   for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
-    Sched<W> sc;
+    Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
     sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
-    if (g.valid) x0 = a.init ? a.init[i * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_OTR);
+    if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_OTR);
     X0Set<W> X0;
     X0.build(g, x0tab[grp], x0);
     // OtrProcess state after init(io) (Otr.scala:15-26); flags are 0/1 lane words
@@ -169,7 +169,8 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
 
 template <int W, bool V2>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((otr_kernel<W, V2>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  if (a.ho_in) hipLaunchKernelGGL((otr_kernel<W, V2, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  else hipLaunchKernelGGL((otr_kernel<W, V2, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -187,10 +188,10 @@ static hipError_t launch_v(const KArgs& a, int W, int grid, hipStream_t s) {
 template <bool V2>
 static const void* ptr_v(int W) {
   switch (W) {
-    case 1: return (const void*)otr_kernel<1, V2>;
-    case 2: return (const void*)otr_kernel<2, V2>;
-    case 3: return (const void*)otr_kernel<3, V2>;
-    case 4: return (const void*)otr_kernel<4, V2>;
+    case 1: return (const void*)otr_kernel<1, V2, false>;
+    case 2: return (const void*)otr_kernel<2, V2, false>;
+    case 3: return (const void*)otr_kernel<3, V2, false>;
+    case 4: return (const void*)otr_kernel<4, V2, false>;
   }
   return nullptr;
 }

@@ -23,7 +23,7 @@ EXPORTED_SYMBOLS = [
     "psg_create", "psg_load_inputs", "psg_run_batch", "psg_copy_decisions",
     "psg_fetch_instances", "psg_last_error", "psg_destroy", "psg_create_error",
     "psg_selftest_map_head", "psg_load_inputs_f64", "psg_copy_decisions_f64", "psg_fetch_instances_f64",
-    "psg_run_batch_spec",
+    "psg_run_batch_spec", "psg_load_schedule", "psg_clear_schedule", "psg_materialize_schedule",
 ]
 
 
@@ -68,6 +68,9 @@ def load():
                                           C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.psg_run_batch_spec.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(abi.SpecProgram),
                                      C.POINTER(abi.Summary), C.POINTER(abi.InstanceSummary)]
+    L.psg_load_schedule.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]
+    L.psg_clear_schedule.argtypes = [C.c_void_p]
+    L.psg_materialize_schedule.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]
     L.psg_selftest_map_head.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
                                         C.POINTER(C.c_int32)]
     _lib = L
@@ -97,6 +100,15 @@ class Context:
 
     def load_inputs(self, inst_begin, count, init=None):
         arr = None
+        if init is not None and hasattr(init, "dtype"):  # numpy fast path
+            import numpy as np
+            a = np.ascontiguousarray(init, dtype=np.float64 if self.real else np.int32)
+            if a.size != count * self.cfg.n:
+                raise ValueError("init must be [count][n]")
+            fn = load().psg_load_inputs_f64 if self.real else load().psg_load_inputs
+            ptr = a.ctypes.data_as(C.POINTER(C.c_double if self.real else C.c_int32))
+            self._check(fn(self._h, inst_begin, count, ptr))
+            return
         if init is not None:
             if self.real:
                 flat = [float(v) for row in init for v in row]
@@ -116,6 +128,45 @@ class Context:
         self._check(load().psg_run_batch(self._h, inst_begin, count, C.byref(s), pi))
         self._last_count = count
         return s, (list(pi) if pi is not None else None)
+
+    def run_batch_np(self, inst_begin, count):
+        """psg_run_batch with the per-instance summaries as a numpy structured array
+        (round_amd.records.SUMMARY_DTYPE)."""
+        import numpy as np
+        from .records import SUMMARY_DTYPE
+        s = abi.Summary()
+        pi = np.zeros(count, SUMMARY_DTYPE)
+        ptr = pi.ctypes.data_as(C.POINTER(abi.InstanceSummary))
+        self._check(load().psg_run_batch(self._h, inst_begin, count, C.byref(s), ptr))
+        self._last_count = count
+        return s, pi
+
+    def copy_decisions_np(self):
+        """(decision, decision_round) of the last batch as numpy [count][n] arrays."""
+        import numpy as np
+        shape = (self._last_count, self.cfg.n)
+        dr = np.zeros(shape, np.int32)
+        pdr = dr.ctypes.data_as(C.POINTER(C.c_int32))
+        if self.real:
+            dec = np.zeros(shape, np.float64)
+            self._check(load().psg_copy_decisions_f64(self._h, dec.ctypes.data_as(C.POINTER(C.c_double)), pdr))
+        else:
+            dec = np.zeros(shape, np.int32)
+            self._check(load().psg_copy_decisions(self._h, dec.ctypes.data_as(C.POINTER(C.c_int32)), pdr))
+        return dec, dr
+
+    def fetch_np(self, ids):
+        """psg_fetch_instances into numpy: (SUMMARY_DTYPE [k], PROCESS_DTYPE [k][n])."""
+        import numpy as np
+        from .records import PROCESS_DTYPE, SUMMARY_DTYPE
+        ids = np.ascontiguousarray(ids, np.uint64)
+        k = int(ids.shape[0])
+        sums = np.zeros(k, SUMMARY_DTYPE)
+        recs = np.zeros((k, self.cfg.n), PROCESS_DTYPE)
+        self._check(load().psg_fetch_instances(self._h, ids.ctypes.data_as(C.POINTER(C.c_uint64)), k,
+                                               sums.ctypes.data_as(C.POINTER(abi.InstanceSummary)),
+                                               recs.ctypes.data_as(C.POINTER(abi.ProcessRecord))))
+        return sums, recs
 
     def run_batch_spec(self, inst_begin, count, program, per_instance=False):
         """psg_run_batch_spec with a compiled Spec (round_amd.formula.Program)."""
@@ -157,6 +208,34 @@ class Context:
         fx = (C.c_double * (k * self.cfg.n))()
         self._check(load().psg_fetch_instances_f64(self._h, arr, k, sums, recs, dec, fx))
         return list(sums), list(recs), list(dec), list(fx)
+
+    def load_schedule(self, inst_begin, count, ho, crash=None):
+        """psg_load_schedule: ho uint64 [count][R][n][W], crash int32 [count][n] or None."""
+        import numpy as np
+        W = (self.cfg.n + 63) // 64
+        ho = np.ascontiguousarray(ho, dtype=np.uint64)
+        if ho.size != count * self.cfg.rounds * self.cfg.n * W:
+            raise ValueError("ho must be [count][rounds][n][W] uint64")
+        cr = None
+        if crash is not None:
+            cr = np.ascontiguousarray(crash, dtype=np.int32)
+            if cr.size != count * self.cfg.n:
+                raise ValueError("crash must be [count][n] int32")
+        self._check(load().psg_load_schedule(self._h, inst_begin, count, ho.ctypes.data_as(C.c_void_p),
+                                             None if cr is None else cr.ctypes.data_as(C.c_void_p)))
+
+    def clear_schedule(self):
+        self._check(load().psg_clear_schedule(self._h))
+
+    def materialize_schedule(self, inst_begin, count):
+        """The seeded schedule: (ho uint64 [count][R][n][W], crash int32 [count][n])."""
+        import numpy as np
+        W = (self.cfg.n + 63) // 64
+        ho = np.zeros((count, self.cfg.rounds, self.cfg.n, W), np.uint64)
+        cr = np.zeros((count, self.cfg.n), np.int32)
+        self._check(load().psg_materialize_schedule(self._h, inst_begin, count, ho.ctypes.data_as(C.c_void_p),
+                                                    cr.ctypes.data_as(C.c_void_p)))
+        return ho, cr
 
     def close(self):
         if getattr(self, "_h", None):

@@ -317,6 +317,18 @@ class GpuRound:
         s, pi = self._ctx.run_batch_spec(inst_begin, count, prog, per_instance)
         return SpecResult(prog.slot_names, self.cfg.rounds, s, pi)
 
+    def load_schedule(self, inst_begin: int, count: int, ho, crash=None):
+        """Explicit HO sets for instances [inst_begin, inst_begin+count): uint64
+        [count][R][n][W] (psg_load_schedule); crash [count][n] marks crashed processes."""
+        self._ctx.load_schedule(inst_begin, count, ho, crash)
+
+    def clear_schedule(self):
+        self._ctx.clear_schedule()
+
+    def materialize_schedule(self, inst_begin: int, count: int):
+        """The seeded HO sets of instances [inst_begin, inst_begin+count), as data."""
+        return self._ctx.materialize_schedule(inst_begin, count)
+
     def decisions(self):
         return self._ctx.copy_decisions()
 
