@@ -76,6 +76,8 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a)
   Grp<W> g;
   grp_setup(g, a, xb, red);
   constexpr int G = Geometry<W>::kGroups;
+  // wave-uniform group index (SGPR): measured +3% on this kernel (fewer VGPRs, one more wave/SIMD);
+  // the same change cost OTR / ShortLastVoting 1-3%, which keep the VGPR form
   const int grp = W == 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
   const int n = a.n;
   const int f = a.param;

@@ -29,7 +29,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
   Grp<W> g;
   grp_setup(g, a, xb, red);
   constexpr int G = Geometry<W>::kGroups;
-  const int grp = W == 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
   const int n = a.n;
   const int f = a.param;
   const Mask<W> full = mfull<W>(n);

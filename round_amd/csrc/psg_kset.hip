@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
   Grp<W> g;
   grp_setup(g, a, xb, red);
   constexpr int G = Geometry<W>::kGroups;
-  const int grp = W == 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
   const int n = a.n;
   const int kk = a.param;
   const int need = a.variant == 1 ? 1 : n - kk;  // same.size > n - k (KSetAgreement.scala:56)

@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
   Grp<W> g;
   grp_setup(g, a, xb, red);
   constexpr int G = Geometry<W>::kGroups;
-  const int grp = W == 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+  const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
   const int n = a.n;
   const int need2 = a.variant == 1 ? 0 : n / 2;  // R2 quorum (ShortLastVoting.scala:85; variant 1: mutation)
   const Mask<W> full = mfull<W>(n);

@@ -16,7 +16,7 @@ import sys
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpsg.so")
+LIB_PATH = os.environ.get("PSG_LIB") or os.path.join(HERE, "libpsg.so")  # PSG_LIB: A/B builds
 
 EXPORTED_SYMBOLS = [
     "psg_config_default", "psg_check_count", "psg_check_name", "psg_alg_from_class",
