@@ -547,6 +547,27 @@ static int validate_prog(const psg_spec_program* p, std::string& m) {
   return PSG_OK;
 }
 
+// Fields a (validated) program reads: FIELD operands and V.exists field sets.
+static uint32_t prog_fields(const psg_spec_program* p) {
+  uint32_t m = 0;
+  for (int pc = 0; pc < p->n_words;) {
+    const int32_t w = p->code[pc];
+    const int op = w & 0xff, a = (w >> 8) & 0xff;
+    if (op == PSG_OP_FIELD) m |= 1u << a;
+    ++pc;
+    if (op == PSG_OP_IMM32) ++pc;
+    if (op == PSG_OP_QBEGIN) {
+      ++pc;
+      if (a == PSG_Q_EXISTS_VI) {
+        const int nf = (p->code[pc] >> 16) & 0xffff;
+        for (int k = 0; k < nf; ++k) m |= 1u << (p->code[pc + 1 + k] & 0xff);
+        pc += 1 + nf;
+      }
+    }
+  }
+  return m & ((1u << PSG_NFIELDS) - 1u);
+}
+
 int psg_copy_decisions(psg_ctx* c, int32_t* decision, int32_t* decision_round) {
   if (!c) return PSG_EINVAL;
   HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -620,6 +641,7 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
     HIPCHK(c, hipModuleGetFunction(&c->native_fn, c->module, name.c_str()));
     c->module_path = prog->module_path;
   }
+  const uint32_t fields = prog_fields(prog);
   psg_summary acc;
   std::memset(&acc, 0, sizeof(acc));
   int vm_grid = 0;
@@ -635,6 +657,7 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
     a.out_dround = c->d_dround + off * (uint64_t)n;
     a.out_inst = c->d_inst + off;
     a.trace = c->d_trace;
+    a.trace_fields = fields;
     psg_summary part;
     int rc = run_kernel(c, a, m_cnt, &part, true);
     if (rc) return rc;

@@ -34,6 +34,7 @@ struct KArgs {
   double* out_rec_f64;               // nullable: [count][n][2] (decision, final x) for the fetch path
   double real_param;                 // EpsilonConsensus epsilon
   int32_t* trace;                    // nullable: Spec-program trace [count][R+1][PSG_NFIELDS][n]
+  uint32_t trace_fields;             // bit f: field f is traced (the fields the Spec program reads)
   int32_t n, R, V, param, param2, variant, tiebreak;
   uint32_t drop_log2, good_p32;
   int32_t good_min, crash_fmax, ho_min;
@@ -780,15 +781,17 @@ PSG_DEV void trace_put(const Grp<W>& g, const KArgs& a, uint64_t i, int c, int32
   if (!g.valid) return;
   const uint64_t n = (uint64_t)a.n;
   int32_t* t = a.trace + (i * (uint64_t)(a.R + 1) + (uint64_t)c) * PSG_NFIELDS * n + (uint64_t)g.pid;
-  t[PSG_FIELD_X * n] = x;
-  t[PSG_FIELD_DECIDED * n] = decided;
-  t[PSG_FIELD_DECISION * n] = decision;
-  t[PSG_FIELD_TS * n] = ts;
-  t[PSG_FIELD_READY * n] = ready;
-  t[PSG_FIELD_COMMIT * n] = commit;
-  t[PSG_FIELD_VOTE * n] = vote;
-  t[PSG_FIELD_CANDECIDE * n] = cand;
-  t[PSG_FIELD_HOSIZE * n] = hosize;
+  // only the fields the program reads (uniform tests): rows of unread fields stay unwritten
+  const uint32_t m = a.trace_fields;
+  if (m & (1u << PSG_FIELD_X)) t[PSG_FIELD_X * n] = x;
+  if (m & (1u << PSG_FIELD_DECIDED)) t[PSG_FIELD_DECIDED * n] = decided;
+  if (m & (1u << PSG_FIELD_DECISION)) t[PSG_FIELD_DECISION * n] = decision;
+  if (m & (1u << PSG_FIELD_TS)) t[PSG_FIELD_TS * n] = ts;
+  if (m & (1u << PSG_FIELD_READY)) t[PSG_FIELD_READY * n] = ready;
+  if (m & (1u << PSG_FIELD_COMMIT)) t[PSG_FIELD_COMMIT * n] = commit;
+  if (m & (1u << PSG_FIELD_VOTE)) t[PSG_FIELD_VOTE * n] = vote;
+  if (m & (1u << PSG_FIELD_CANDECIDE)) t[PSG_FIELD_CANDECIDE * n] = cand;
+  if (m & (1u << PSG_FIELD_HOSIZE)) t[PSG_FIELD_HOSIZE * n] = hosize;
 }
 
 // Group geometry: W == 1 -> 4 independent instances per 256-thread block;

@@ -70,11 +70,15 @@ PSG_DEV int32_t count_lane(Ctx<W>& x, Fn fn) {
 }
 
 // ---------------------------------------------------------------- process quantifiers, serial form
+// Bodies are evaluated on every lane (converged): a body may hold ballots and
+// cross-lane reads, which need all lanes; a per-lane short circuit would not
+// save issue slots anyway (the wave runs the body while any lane needs it).
 template <int W, class Fn>
 PSG_DEV int32_t forall_ser(Ctx<W>& x, Fn fn) {
   int32_t acc = 1;
   for (int j = 0; j < x.n; ++j) {
-    acc = (acc != 0 && fn(j) != 0) ? 1 : 0;
+    const int32_t b = fn(j);
+    acc = (acc != 0 && b != 0) ? 1 : 0;
     if (!x.g.any(acc != 0)) break;
   }
   return acc;
@@ -83,7 +87,8 @@ template <int W, class Fn>
 PSG_DEV int32_t exists_ser(Ctx<W>& x, Fn fn) {
   int32_t acc = 0;
   for (int j = 0; j < x.n; ++j) {
-    acc = (acc != 0 || fn(j) != 0) ? 1 : 0;
+    const int32_t b = fn(j);
+    acc = (acc != 0 || b != 0) ? 1 : 0;
     if (!x.g.any(acc == 0)) break;
   }
   return acc;
@@ -95,28 +100,103 @@ PSG_DEV int32_t count_ser(Ctx<W>& x, Fn fn) {
   return acc;
 }
 
+// ---------------------------------------------------------------- serial form over distinct states
+// A nested process quantifier whose body reads its variable j only through fields
+// visits each distinct tuple of those fields once instead of every pid: forall /
+// exists are insensitive to repeats, count weighs a tuple by how many processes
+// hold it (a popcount). Typically 1-3 tuples (e.g. undecided / decided v) vs n.
+template <int F, int T>
+struct Fld {
+  static constexpr int f = F, tag = T;
+};
+
+template <int W, int MODE, class Fn, class... Fs>  // MODE 0 forall, 1 exists, 2 count
+PSG_DEV int32_t quant_tup(Ctx<W>& x, Fn fn, Fs...) {
+  int32_t acc = MODE == 0 ? 1 : 0;
+  Mask<W> rem = x.g.ballot(true);
+  while (many(rem)) {
+    const int q = mfirst(rem);
+    Mask<W> E = rem;
+    auto val = [&](auto fld) -> int32_t {
+      using FL = decltype(fld);
+      const int32_t mine = x.own(FL::tag, FL::f);
+      const int32_t v = x.g.bcast(mine, x.stage(FL::tag, FL::f), q);
+      E = mand(E, x.g.ballot(mine == v));
+      return v;
+    };
+    const int32_t b = fn(val(Fs{})...);
+    rem = mandn(rem, E);
+    if constexpr (MODE == 0) {
+      acc = (acc != 0 && b != 0) ? 1 : 0;
+      if (!x.g.any(acc != 0)) break;
+    } else if constexpr (MODE == 1) {
+      acc = (acc != 0 || b != 0) ? 1 : 0;
+      if (!x.g.any(acc == 0)) break;
+    } else {
+      acc += b != 0 ? mpopc(E) : 0;
+    }
+  }
+  return acc;
+}
+
+// ---------------------------------------------------------------- connectives with an expensive right side
+// a && b, a || b, a ==> b where b holds a quantifier: b is skipped when no lane of
+// the group needs it (a group-uniform decision, so b still runs converged).
+template <int W, class Fn>
+PSG_DEV int32_t and_sc(Ctx<W>& x, int32_t a, Fn fb) {
+  if (!x.g.any(a != 0)) return 0;
+  const int32_t b = fb();
+  return (a != 0 && b != 0) ? 1 : 0;
+}
+template <int W, class Fn>
+PSG_DEV int32_t or_sc(Ctx<W>& x, int32_t a, Fn fb) {
+  if (!x.g.any(a == 0)) return 1;
+  const int32_t b = fb();
+  return (a != 0 || b != 0) ? 1 : 0;
+}
+template <int W, class Fn>
+PSG_DEV int32_t impl_sc(Ctx<W>& x, int32_t a, Fn fb) {
+  if (!x.g.any(a != 0)) return 1;
+  const int32_t b = fb();
+  return (a == 0 || b != 0) ? 1 : 0;
+}
+
 // ---------------------------------------------------------------- value domains
 template <int W, class Fn>
 PSG_DEV int32_t exists_bool(Ctx<W>& x, Fn fn) {
   int32_t acc = fn(0) != 0 ? 1 : 0;
-  if (x.g.any(acc == 0)) acc = (acc != 0 || fn(1) != 0) ? 1 : 0;
+  if (x.g.any(acc == 0)) {
+    const int32_t b = fn(1);
+    acc = (acc != 0 || b != 0) ? 1 : 0;
+  }
   return acc;
 }
 
 // V.exists over Int. Candidate sources: per-lane expression values `ev[0..ne)`
 // (their distinct values over the lanes) and field sets `fs[0..nf)` (field | tag
 // << 8: the distinct values of that field over all processes); each value v
-// contributes v-1, v, v+1; then Int.MinValue and Int.MaxValue.
-template <int W, class Fn>
+// contributes v-1, v, v+1 (EQ: v only); then Int.MinValue and Int.MaxValue
+// (EQ: one value outside the candidate set).
+template <int W, class Fn, bool EQ = false>
 struct ExistsInt {
   Ctx<W>& x;
   Fn& fn;
   int32_t acc;
+  int32_t lo, hi;  // extreme candidate values visited (EQ)
+  bool any_v;
   PSG_DEV bool done() { return !x.g.any(acc == 0); }
+  PSG_DEV void test(int32_t cand) {
+    const int32_t b = fn(cand);
+    acc = (acc != 0 || b != 0) ? 1 : 0;
+  }
   PSG_DEV void visit(int32_t v) {
-    for (int d = -1; d <= 1; ++d) {
-      const int32_t cand = (int32_t)((uint32_t)v + (uint32_t)d);
-      acc = (acc != 0 || fn(cand) != 0) ? 1 : 0;
+    if constexpr (EQ) {
+      test(v);
+      lo = any_v && lo < v ? lo : v;
+      hi = any_v && hi > v ? hi : v;
+      any_v = true;
+    } else {
+      for (int d = -1; d <= 1; ++d) test((int32_t)((uint32_t)v + (uint32_t)d));
     }
   }
   // distinct values of the per-lane `val` over the lanes in `m`
@@ -131,10 +211,9 @@ struct ExistsInt {
   }
 };
 
-template <int W, int NE, int NF, class Fn>
-PSG_DEV int32_t exists_int(Ctx<W>& x, const int32_t (&ev)[NE > 0 ? NE : 1], const int32_t (&fs)[NF > 0 ? NF : 1],
-                           int32_t* scratch, Fn fn) {
-  ExistsInt<W, Fn> e{x, fn, 0};
+template <int W, int NE, int NF, class Fn, bool EQ>
+PSG_DEV bool exists_int_scan(ExistsInt<W, Fn, EQ>& e, Ctx<W>& x, const int32_t (&ev)[NE > 0 ? NE : 1],
+                             const int32_t (&fs)[NF > 0 ? NF : 1], int32_t* scratch) {
   const Mask<W> all = x.g.ballot(true);
   for (int k = 0; k < NE; ++k) {
     if constexpr (W > 1) {
@@ -143,15 +222,64 @@ PSG_DEV int32_t exists_int(Ctx<W>& x, const int32_t (&ev)[NE > 0 ? NE : 1], cons
     }
     const bool d = e.over(ev[k], all, scratch);
     if constexpr (W > 1) __syncthreads();
-    if (d) return e.acc;
+    if (d) return true;
   }
   for (int k = 0; k < NF; ++k) {
     const int f = fs[k] & 0xff, tag = (fs[k] >> 8) & 0xff;
-    if (e.over(x.own(tag, f), all, x.stage(tag, f))) return e.acc;
+    if (e.over(x.own(tag, f), all, x.stage(tag, f))) return true;
   }
-  e.acc = (e.acc != 0 || fn(INT32_MIN) != 0) ? 1 : 0;
-  e.acc = (e.acc != 0 || fn(INT32_MAX) != 0) ? 1 : 0;
+  return false;
+}
+
+template <int W, int NE, int NF, class Fn>
+PSG_DEV int32_t exists_int(Ctx<W>& x, const int32_t (&ev)[NE > 0 ? NE : 1], const int32_t (&fs)[NF > 0 ? NF : 1],
+                           int32_t* scratch, Fn fn) {
+  ExistsInt<W, Fn, false> e{x, fn, 0, 0, 0, false};
+  if (exists_int_scan<W, NE, NF>(e, x, ev, fs, scratch)) return e.acc;
+  e.test(INT32_MIN);
+  e.test(INT32_MAX);
   return e.acc;
+}
+
+// V.exists over Int whose variable is only compared with == / != : the body has
+// one truth value on all values outside the candidate set W, so the candidates
+// plus ONE value outside W decide it (max+1 or min-1; when W holds both Int
+// extremes, the general +-1 finitization).
+template <int W, int NE, int NF, class Fn>
+PSG_DEV int32_t exists_int_eq(Ctx<W>& x, const int32_t (&ev)[NE > 0 ? NE : 1],
+                              const int32_t (&fs)[NF > 0 ? NF : 1], int32_t* scratch, Fn fn) {
+  ExistsInt<W, Fn, true> e{x, fn, 0, 0, 0, false};
+  if (exists_int_scan<W, NE, NF>(e, x, ev, fs, scratch)) return e.acc;
+  if (!e.any_v) e.test(0);
+  else if (e.hi != INT32_MAX) e.test(e.hi + 1);
+  else if (e.lo != INT32_MIN) e.test(e.lo - 1);
+  else return exists_int<W, NE, NF>(x, ev, fs, scratch, fn);
+  return e.acc;
+}
+
+// V.exists(v => ... && P.filter(i => i.t == v).size >= L && ...): a witness v is
+// a value of the per-process term t held by at least L processes. With 2L > n
+// that is the strict majority (Boyer-Moore candidate, one body evaluation);
+// otherwise the distinct values of t filtered by their count. Requires L >= 1.
+template <int W, class Fn>
+PSG_DEV int32_t exists_int_guard(Ctx<W>& x, int32_t t, const int32_t* staged, int32_t L, Fn fn) {
+  if (2 * (int64_t)L > (int64_t)x.n) {
+    const int32_t m = majority_candidate<W>(x.g, t);
+    if (mpopc(x.g.ballot(t == m)) < L) return 0;
+    return fn(m) != 0 ? 1 : 0;
+  }
+  int32_t acc = 0;
+  Mask<W> rem = x.g.ballot(true);
+  while (many(rem)) {
+    const int32_t v = x.g.bcast(t, staged, mfirst(rem));
+    const Mask<W> E = x.g.ballot(t == v);
+    rem = mandn(rem, E);
+    if (mpopc(E) < L) continue;
+    const int32_t b = fn(v);
+    acc = (acc != 0 || b != 0) ? 1 : 0;
+    if (!x.g.any(acc == 0)) break;
+  }
+  return acc;
 }
 
 // ---------------------------------------------------------------- arithmetic with Scala Int semantics

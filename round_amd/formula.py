@@ -690,6 +690,7 @@ class _Gen:
         self.tags = set()
         self.fields_available = fields_available
         self.max_vi = 0
+        self.tuples = {}      # var uid -> {(field, tag): C++ name} (serial quantifier over distinct states)
 
     def gen(self, e, in_lane, vi_depth):
         """(C++ expression, depends on the lane)."""
@@ -713,6 +714,8 @@ class _Gen:
             self.tags.add(e.tag)
             if isinstance(e.proc, Var) and self.names.get(e.proc.uid, (None, False, False))[2]:
                 return f"x.own({e.tag}, {e.f})", True  # the lane's own process
+            if isinstance(e.proc, Var) and e.proc.uid in self.tuples:
+                return self.tuples[e.proc.uid][(e.f, e.tag)], False  # a distinct-state tuple value
             p, lane = self.gen(e.proc, in_lane, vi_depth)
             fn = "fld_g" if lane else "fld_u"
             return f"spec::{fn}<W>(x, {e.tag}, {e.f}, {p})", lane
@@ -726,6 +729,15 @@ class _Gen:
         if isinstance(e, Bin):
             a, la = self.gen(e.x, in_lane, vi_depth)
             b, lb = self.gen(e.y, in_lane, vi_depth)
+            if e.op in ("AND", "OR", "IMPL") and _expensive(e.y):
+                # skip a quantified right side when no lane needs it (group-uniform test)
+                if not la:
+                    t = {"AND": "({a}) != 0 ? (int32_t)(({b}) != 0) : 0",
+                         "OR": "({a}) != 0 ? 1 : (int32_t)(({b}) != 0)",
+                         "IMPL": "({a}) == 0 ? 1 : (int32_t)(({b}) != 0)"}[e.op]
+                    return "(" + t.format(a=a, b=b) + ")", lb
+                fn = {"AND": "and_sc", "OR": "or_sc", "IMPL": "impl_sc"}[e.op]
+                return f"spec::{fn}<W>(x, {a}, [&]() -> int32_t {{ return {b}; }})", True
             return self.BIN[e.op].format(x=a, y=b), la or lb
         if isinstance(e, Contains):
             val, lane = self.gen(e.e, in_lane, vi_depth)
@@ -745,6 +757,23 @@ class _Gen:
                 body, _ = self.gen(q.body, True, vi_depth)
                 fn = {"forall": "forall_lane", "exists": "exists_lane", "count": "count_lane"}[q.kind]
                 return f"spec::{fn}<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", False
+            flds = _tuple_fields(q)
+            if flds is not None:
+                # the body reads j only through fields: visit each distinct field tuple once
+                # (count: weighted by how many processes hold it)
+                names = {ft: f"{v}_{k}" for k, ft in enumerate(flds)}
+                self.tuples[q.var.uid] = names
+                for f, tag in flds:
+                    if self.fields_available is not None and f not in self.fields_available:
+                        raise FormulaError(f"field {f} is not part of this algorithm's state")
+                    self.fields.add(f)
+                    self.tags.add(tag)
+                body, lane = self.gen(q.body, in_lane, vi_depth)
+                mode = {"forall": 0, "exists": 1, "count": 2}[q.kind]
+                params = ", ".join(f"int32_t {names[ft]}" for ft in flds)
+                fl = ", ".join(f"spec::Fld<{f}, {tag}>{{}}" for f, tag in flds)
+                return (f"spec::quant_tup<W, {mode}>(x, [&]({params}) -> int32_t {{ return {body}; }}"
+                        f"{', ' if fl else ''}{fl})"), lane
             self.names[q.var.uid] = (v, False, False)
             body, lane = self.gen(q.body, in_lane, vi_depth)
             fn = {"forall": "forall_ser", "exists": "exists_ser", "count": "count_ser"}[q.kind]
@@ -753,7 +782,32 @@ class _Gen:
         if q.kind == "vbool":
             body, lane = self.gen(q.body, in_lane, vi_depth)
             return f"spec::exists_bool<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", lane
+        guard = _count_guard(q)
+        if guard is not None:
+            # a conjunct P.filter(i => i.f == v).size >= L restricts the witnesses to values
+            # of f held by >= L processes (runtime L >= 1; else the general finitization)
+            (f, tag), thr, op = guard
+            self.fields.add(f)
+            self.tags.add(tag)
+            tc, tl = self.gen(thr, in_lane, vi_depth)
+            if tl:
+                guard = None
+        if guard is not None:
+            L = f"(({tc}) + 1)" if op == "GT" else f"({tc})"
+            general, lane_g = self._vint_general(q, v, in_lane, vi_depth)
+            self.names[q.var.uid] = (v, False, False)
+            body, lane = self.gen(q.body, in_lane, vi_depth + 1)
+            self.max_vi = max(self.max_vi, vi_depth + 1)
+            return (f"([&]() -> int32_t {{ const int32_t L_ = {L}; if (L_ >= 1) return "
+                    f"spec::exists_int_guard<W>(x, x.own({tag}, {f}), x.stage({tag}, {f}), L_, "
+                    f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); return {general}; }})()"), True
+        return self._vint_general(q, v, in_lane, vi_depth)
+
+    def _vint_general(self, q, v, in_lane, vi_depth):
+        """V.exists over Int by finitization over the compared terms (equality-only: no +-1)."""
+        self.names[q.var.uid] = (v, False, False)
         exprs, fsets = _Compiler.witnesses(_Compiler(), q)
+        eq_only = _eq_only(q)
         evs = []
         for t in exprs:
             c, _ = self.gen(t, in_lane, vi_depth)
@@ -766,10 +820,76 @@ class _Gen:
         ne, nf = len(evs), len(fsets)
         ev = ", ".join(evs) if evs else "0"
         fs = ", ".join(str(f | (t << 8)) for f, t in fsets) if fsets else "0"
+        fn = "exists_int_eq" if eq_only else "exists_int"
         return (f"([&]() -> int32_t {{ const int32_t ev_[{max(ne, 1)}] = {{{ev}}}; "
                 f"const int32_t fs_[{max(nf, 1)}] = {{{fs}}}; "
-                f"return spec::exists_int<W, {ne}, {nf}>(x, ev_, fs_, scratch + {vi_depth} * 64 * W, "
+                f"return spec::{fn}<W, {ne}, {nf}>(x, ev_, fs_, scratch + {vi_depth} * 64 * W, "
                 f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); }})()"), True
+
+
+def _expensive(e) -> bool:
+    """Does e hold a quantifier or a set membership (worth a short circuit)?"""
+    return any(isinstance(x, (Quant, Contains)) for x in _walk(e))
+
+
+def _tuple_fields(q):
+    """Fields (field, tag) through which the body of a process quantifier reads its
+    variable, or None if the variable is used otherwise (compared as a pid, bound by
+    a set membership, ...)."""
+    uid = q.var.uid
+    out = []
+    field_procs = set()
+    for x in _walk(q.body):
+        if isinstance(x, Field) and isinstance(x.proc, Var) and x.proc.uid == uid:
+            field_procs.add(id(x.proc))
+            if (x.f, x.tag) not in out:
+                out.append((x.f, x.tag))
+    for x in _walk(q.body):
+        if isinstance(x, Var) and x.uid == uid and id(x) not in field_procs:
+            return None
+    return out if len(out) <= 4 else None
+
+
+def _conjuncts(e):
+    if isinstance(e, Bin) and e.op == "AND":
+        return _conjuncts(e.x) + _conjuncts(e.y)
+    return [e]
+
+
+def _eq_only(q) -> bool:
+    """Is the V.exists variable of q compared with == / != only?"""
+    uid = q.var.uid
+    for x in _walk(q.body):
+        if isinstance(x, Bin) and x.op in ("LT", "LE", "GT", "GE"):
+            for a in (x.x, x.y):
+                if isinstance(a, Var) and a.uid == uid:
+                    return False
+    return True
+
+
+def _count_guard(q):
+    """A top-level conjunct `P.filter(i => i.f == v).size OP thr` (OP in >, >=, ==; thr
+    free of bound variables) of V.exists(v => body): ((f, tag), thr, OP) or None."""
+    uid = q.var.uid
+    for c in _conjuncts(q.body):
+        if not isinstance(c, Bin) or c.op not in ("GT", "GE", "EQ", "LT", "LE"):
+            continue
+        cnt, thr, op = c.x, c.y, c.op
+        if not (isinstance(cnt, Quant) and cnt.kind == "count"):
+            cnt, thr = c.y, c.x
+            op = {"LT": "GT", "LE": "GE", "EQ": "EQ", "GT": "LT", "GE": "LE"}[c.op]
+        if op not in ("GT", "GE", "EQ") or not (isinstance(cnt, Quant) and cnt.kind == "count"):
+            continue
+        if any(isinstance(x, (Var, Quant, Field, Contains)) for x in _walk(thr)):
+            continue  # the threshold must be uniform (n, r, literals)
+        b = cnt.body
+        if not (isinstance(b, Bin) and b.op == "EQ"):
+            continue
+        for fld, other in ((b.x, b.y), (b.y, b.x)):
+            if (isinstance(fld, Field) and isinstance(fld.proc, Var) and fld.proc.uid == cnt.var.uid
+                    and isinstance(other, Var) and other.uid == uid):
+                return (fld.f, fld.tag), thr, op
+    return None
 
 
 def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:

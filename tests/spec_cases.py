@@ -45,6 +45,24 @@ def benor_custom():
         ])
 
 
+def witness_shapes():
+    """V.exists shapes the native lowering specializes: a count guard with a
+    non-majority threshold (enumeration filtered by count), a guard whose runtime
+    threshold is < 1 (general finitization), equality-only variables (one value
+    outside the candidates), and a guard under a lane quantifier."""
+    return F.Spec(properties=[
+        ("GuardLow", V.exists(lambda v: (P.filter(lambda i: i.x == v).size >= 2)
+                              & P.exists(lambda j: j.decided & (j.decision == v)))),
+        ("GuardVacuous", V.exists(lambda v: (P.filter(lambda i: i.x == v).size > n - 1000)
+                                  & P.forall(lambda j: j.decided.implies(j.decision == v)))),
+        ("EqFresh", V.exists(lambda v: P.forall(lambda i: i.decided.implies(i.decision != v)))),
+        ("EqNone", V.exists(lambda v: P.forall(lambda i: (i.x == v) | (i.decision != v)))),
+        ("GuardInLane", P.forall(lambda i: i.decided.implies(V.exists(lambda v: (
+            n // 2 < P.filter(lambda j: j.x == v).size) & (i.decision == v))))),
+        ("GuardEqN", V.exists(lambda v: (P.filter(lambda i: old(i.x) == v).size == n) & (r > 0))),
+    ])
+
+
 # (id, algorithm, n, make_config kwargs, spec factory)
 CUSTOM = [
     ("fm-n12", psync.FloodMin(2), 12, dict(value_range=8, schedule=H(drop_log2=0, good_round=0.0, crash_fmax=3)),
@@ -59,4 +77,8 @@ CUSTOM = [
     ("slv-n16", psync.ShortLastVoting(), 16, dict(value_range=4), uniform_agreement),
     ("benor-n8", psync.BenOr(), 8, {}, benor_custom),
     ("otr2-n12", psync.OTR2(), 12, dict(value_range=4), uniform_agreement),
+    ("otr-n16-shapes", psync.OTR(), 16, dict(value_range=3), witness_shapes),
+    ("otr2-n100-shapes", psync.OTR2(), 100, dict(value_range=3), witness_shapes),
+    ("fm-n8-shapes", psync.FloodMin(2), 8, dict(value_range=3, schedule=H(drop_log2=0, good_round=0.0,
+                                                                           crash_fmax=3)), witness_shapes),
 ]
