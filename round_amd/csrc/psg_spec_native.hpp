@@ -33,6 +33,7 @@ struct Ctx {
   int32_t o[PSG_NFIELDS];
   int32_t i[PSG_NFIELDS];
   int32_t* sc;             // W > 1: staged copies [3][PSG_NFIELDS][64W]
+  X0Set<W> iset[2];        // membership sets of init(field) values (S::kInitSet0 / kInitSet1)
   PSG_DEV const int32_t* stage(int tag, int f) const { return sc + (tag * PSG_NFIELDS + f) * 64 * W; }
   PSG_DEV int32_t own(int tag, int f) const { return tag == PSG_TAG_CUR ? c[f] : (tag == PSG_TAG_OLD ? o[f] : i[f]); }
 };
@@ -137,6 +138,14 @@ PSG_DEV int32_t quant_tup(Ctx<W>& x, Fn fn, Fs...) {
     }
   }
   return acc;
+}
+
+// P.exists(j => init(j.f) == t): membership of t in the instance's set of initial
+// values of f — an LDS hash set built once per instance (X0Set), as the
+// hand-lowered checks do, instead of a loop over the processes.
+template <int W, int K>
+PSG_DEV int32_t member_init(Ctx<W>& x, int32_t t) {
+  return (int32_t)x.iset[K].contains01(t);
 }
 
 // ---------------------------------------------------------------- connectives with an expensive right side
@@ -300,6 +309,8 @@ __device__ void native_kernel_body(const VmArgs& A) {
   __shared__ int64_t red[2 * W];
   __shared__ int32_t stg[W > 1 ? 3 * PSG_NFIELDS * 64 * W : 1];
   __shared__ int32_t scratch[Geometry<W>::kGroups][64 * W];
+  __shared__ int32_t isets[S::kInitSet0 >= 0 ? (S::kInitSet1 >= 0 ? 2 : 1) : 1][Geometry<W>::kGroups]
+                          [S::kInitSet0 >= 0 ? X0Set<W>::kSlots : 1];
   counters_init(&bc);
   __syncthreads();
   KArgs ka;
@@ -322,6 +333,8 @@ __device__ void native_kernel_body(const VmArgs& A) {
       }
     };
     load(x.i, base, PSG_TAG_INIT);
+    if constexpr (S::kInitSet0 >= 0) x.iset[0].build(g, isets[0][grp], x.i[S::kInitSet0]);
+    if constexpr (S::kInitSet1 >= 0) x.iset[1].build(g, isets[1][grp], x.i[S::kInitSet1]);
     Checks ck;
     ck.reset();
     for (int c = 0; c <= A.R; ++c) {

@@ -691,6 +691,7 @@ class _Gen:
         self.fields_available = fields_available
         self.max_vi = 0
         self.tuples = {}      # var uid -> {(field, tag): C++ name} (serial quantifier over distinct states)
+        self.init_sets = []   # fields f with an LDS membership set of init(f) (at most 2)
 
     def gen(self, e, in_lane, vi_depth):
         """(C++ expression, depends on the lane)."""
@@ -757,6 +758,15 @@ class _Gen:
                 body, _ = self.gen(q.body, True, vi_depth)
                 fn = {"forall": "forall_lane", "exists": "exists_lane", "count": "count_lane"}[q.kind]
                 return f"spec::{fn}<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", False
+            mem = _init_member(q)
+            if mem is not None and (mem[0] in self.init_sets or len(self.init_sets) < 2):
+                f, t = mem
+                if f not in self.init_sets:
+                    self.init_sets.append(f)
+                self.fields.add(f)
+                self.tags.add(TAG_INIT)
+                tc, tl = self.gen(t, in_lane, vi_depth)
+                return f"spec::member_init<W, {self.init_sets.index(f)}>(x, {tc})", tl
             flds = _tuple_fields(q)
             if flds is not None:
                 # the body reads j only through fields: visit each distinct field tuple once
@@ -830,6 +840,18 @@ class _Gen:
 def _expensive(e) -> bool:
     """Does e hold a quantifier or a set membership (worth a short circuit)?"""
     return any(isinstance(x, (Quant, Contains)) for x in _walk(e))
+
+
+def _init_member(q):
+    """P.exists(j => init(j.f) == t) with t free of j: (f, t), else None."""
+    if q.kind != "exists" or not (isinstance(q.body, Bin) and q.body.op == "EQ"):
+        return None
+    uid = q.var.uid
+    for a, b in ((q.body.x, q.body.y), (q.body.y, q.body.x)):
+        if (isinstance(a, Field) and a.tag == TAG_INIT and isinstance(a.proc, Var) and a.proc.uid == uid
+                and uid not in {x.uid for x in _walk(b) if isinstance(x, Var)}):
+            return a.f, b
+    return None
 
 
 def _tuple_fields(q):
@@ -937,6 +959,8 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
         f"  static constexpr bool kHasTerm = {'true' if term else 'false'};",
         f"  static constexpr uint32_t kFields = {fmask}u;",
         f"  static constexpr uint32_t kTags = {tmask}u;",
+        f"  static constexpr int kInitSet0 = {gen.init_sets[0] if len(gen.init_sets) > 0 else -1};",
+        f"  static constexpr int kInitSet1 = {gen.init_sets[1] if len(gen.init_sets) > 1 else -1};",
         "  template <int W>",
         "  __device__ static uint32_t fail(spec::Ctx<W>& x, int32_t* scratch) {",
         "    (void)scratch;",

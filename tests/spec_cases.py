@@ -60,6 +60,11 @@ def witness_shapes():
         ("GuardInLane", P.forall(lambda i: i.decided.implies(V.exists(lambda v: (
             n // 2 < P.filter(lambda j: j.x == v).size) & (i.decision == v))))),
         ("GuardEqN", V.exists(lambda v: (P.filter(lambda i: old(i.x) == v).size == n) & (r > 0))),
+        # three init-membership sets: two LDS sets, the third falls back to the tuple loop
+        ("Members", P.forall(lambda i: P.exists(lambda j: init(j.x) == i.x)
+                             & P.exists(lambda j: init(j.decided) == i.decided)
+                             & P.exists(lambda j: i.decision == init(j.decision)))),
+        ("MemberUniform", P.exists(lambda j: init(j.x) == r + 1)),
     ])
 
 
