@@ -168,6 +168,45 @@ JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_copyDecisionsF64(JNIE
   if (rc) throw_psg(env, rc, psg_last_error(ctx));
 }
 
+/* void loadSchedule(long ctx, long begin, long count, long[] ho, int[] crashOrNull) —
+ * explicit HO sets [count][R][n][W] (psg_load_schedule) */
+JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_loadSchedule(JNIEnv* env, jobject self, jlong h,
+                                                                        jlong begin, jlong count, jlongArray ho,
+                                                                        jintArray crash) {
+  (void)self;
+  psg_ctx* ctx = (psg_ctx*)(intptr_t)h;
+  jlong* p = (*env)->GetLongArrayElements(env, ho, NULL);
+  jint* c = crash ? (*env)->GetIntArrayElements(env, crash, NULL) : NULL;
+  int rc = psg_load_schedule(ctx, (uint64_t)begin, (uint64_t)count, (const uint64_t*)p, (const int32_t*)c);
+  if (c) (*env)->ReleaseIntArrayElements(env, crash, c, JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, ho, p, JNI_ABORT);
+  if (rc) throw_psg(env, rc, psg_last_error(ctx));
+}
+
+/* void clearSchedule(long ctx) — back to seeded HO sets */
+JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_clearSchedule(JNIEnv* env, jobject self, jlong h) {
+  (void)self;
+  psg_ctx* ctx = (psg_ctx*)(intptr_t)h;
+  int rc = psg_clear_schedule(ctx);
+  if (rc) throw_psg(env, rc, psg_last_error(ctx));
+}
+
+/* void materializeSchedule(long ctx, long begin, long count, long[] ho, int[] crash) — the seeded
+ * HO sets as data, [count][R][n][W] and [count][n] (psg_materialize_schedule): what the in-JVM
+ * harness (integration/scala/HoHarness.scala) replays through the reference's own rounds */
+JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_materializeSchedule(JNIEnv* env, jobject self, jlong h,
+                                                                               jlong begin, jlong count,
+                                                                               jlongArray ho, jintArray crash) {
+  (void)self;
+  psg_ctx* ctx = (psg_ctx*)(intptr_t)h;
+  jlong* p = (*env)->GetLongArrayElements(env, ho, NULL);
+  jint* c = crash ? (*env)->GetIntArrayElements(env, crash, NULL) : NULL;
+  int rc = psg_materialize_schedule(ctx, (uint64_t)begin, (uint64_t)count, (uint64_t*)p, (int32_t*)c);
+  if (c) (*env)->ReleaseIntArrayElements(env, crash, c, 0);
+  (*env)->ReleaseLongArrayElements(env, ho, p, 0);
+  if (rc) throw_psg(env, rc, psg_last_error(ctx));
+}
+
 JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_destroy(JNIEnv* env, jobject self, jlong h) {
   (void)env;
   (void)self;

@@ -24,6 +24,9 @@ object GpuRoundNative {
   @native def runBatch(ctx: Long, begin: Long, count: Long, perInstance: Array[Byte]): Array[Long]
   @native def copyDecisions(ctx: Long, decision: Array[Int], decisionRound: Array[Int]): Unit
   @native def fetch(ctx: Long, ids: Array[Long], sums: Array[Byte], records: Array[Int]): Unit
+  @native def loadSchedule(ctx: Long, begin: Long, count: Long, ho: Array[Long], crash: Array[Int]): Unit
+  @native def clearSchedule(ctx: Long): Unit
+  @native def materializeSchedule(ctx: Long, begin: Long, count: Long, ho: Array[Long], crash: Array[Int]): Unit
   @native def destroy(ctx: Long): Unit
 }
 
@@ -92,6 +95,45 @@ object GpuRound {
         }
       }
       res
+    } finally GpuRoundNative.destroy(ctx)
+  }
+
+  /** The seeded HO sets of instances [begin, begin+count) as data: ho(((i*R + k)*n + p)*W + w) = word w
+    * of HO(p) in round k (bit q: p hears q), crash(i*n + p) = crash round or -1. */
+  def materialize(alg: Algorithm[_, _], cfg: GpuConfig, begin: Long, count: Long): (Array[Long], Array[Int]) = {
+    val W = (cfg.n + 63) / 64
+    val ho = new Array[Long]((count * cfg.rounds * cfg.n * W).toInt)
+    val crash = new Array[Int]((count * cfg.n).toInt)
+    val ctx = create(algId(alg), cfg.copy(batchCapacity = math.max(1L, count)))
+    try GpuRoundNative.materializeSchedule(ctx, begin, count, ho, crash)
+    finally GpuRoundNative.destroy(ctx)
+    (ho, crash)
+  }
+
+  /** Run instances under explicit HO sets (psg_load_schedule): a counterexample file's schedule,
+    * or any schedule built in the JVM. */
+  def runExplicit(alg: Algorithm[_, _], cfg: GpuConfig, begin: Long, count: Long, ho: Array[Long],
+                  crash: Option[Array[Int]] = None, init: Option[Array[Int]] = None): GpuResult = {
+    val ctx = create(algId(alg), cfg)
+    try {
+      GpuRoundNative.loadInputs(ctx, begin, count, init.orNull)
+      GpuRoundNative.loadSchedule(ctx, begin, count, ho, crash.orNull)
+      summary(GpuRoundNative.runBatch(ctx, begin, count, null), cfg.rounds)
+    } finally GpuRoundNative.destroy(ctx)
+  }
+
+  /** Per-process (decision, decisionRound, haltRound, finalX), 4 ints each, of instances
+    * [begin, begin+count) (psg_fetch_instances) with the given initial values (else seeded). */
+  def records(alg: Algorithm[_, _], cfg: GpuConfig, begin: Long, count: Int,
+              init: Option[Array[Int]] = None): Array[Int] = {
+    val ctx = create(algId(alg), cfg.copy(batchCapacity = math.max(1L, count.toLong)))
+    try {
+      if (init.isDefined) GpuRoundNative.loadInputs(ctx, begin, count, init.get)
+      val ids = Array.tabulate(count)(i => begin + i)
+      val sums = new Array[Byte](24 * count)
+      val recs = new Array[Int](4 * cfg.n * count)
+      GpuRoundNative.fetch(ctx, ids, sums, recs)
+      recs
     } finally GpuRoundNative.destroy(ctx)
   }
 
