@@ -50,7 +50,7 @@ def parse():
 
 
 def pmc_traffic_bytes(args):
-    """HBM bytes per launch of otr_kernel<1, false> from the newest committed PMC summary
+    """HBM bytes per launch of otr_kernel<1, false, false> from the newest committed PMC summary
     (profiles/*/pmc_summary.json, scripts/summarize_profile.py) of this exact workload."""
     import glob
     best = None
@@ -182,7 +182,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": "psg::otr_kernel<1, false>",
+                "kernel": "psg::otr_kernel<1, false, false>",  # <W, OTR2, explicit schedule>
                 "kernel_ms": head["kernel_s"] * 1e3,
                 "bytes_per_process_round": B_ALG_OTR,
             },
