@@ -315,6 +315,35 @@ int psg_clear_schedule(psg_ctx* ctx);
 int psg_materialize_schedule(psg_ctx* ctx, uint64_t inst_begin, uint64_t inst_count, uint64_t* ho,
                              int32_t* crash_round);
 
+/* Device-resident search populations: the adversary search's generate /
+ * mutate step (round_amd/adversary.py) on the GPU, so HO sets never cross PCIe.
+ * A population is the loaded explicit schedule + the staged initial values of
+ * [inst_begin, inst_begin+count); general-omission fault model (every link of
+ * every round independently present or not). All draws are Philox4x32-10 keyed
+ * by `seed` with the generation number in the counter, so a population is a
+ * pure function of its parameters. */
+typedef struct psg_population_params {
+  uint64_t seed;            /* generator key */
+  uint32_t generation;      /* distinct draws per generation */
+  uint32_t flips;           /* links (k, p, q) flipped per mutant (q != p when self_bit) */
+  int32_t min_size;         /* repair: |HO(p)| >= min_size after generation / mutation (<= 0: none);
+                               BenOr safetyPredicate |HO(p)| > n/2 (BenOr.scala:92) = n/2 + 1 */
+  uint32_t self_bit;        /* p in HO(p) (psync/Round.scala:114-116) */
+  uint32_t keep_p256[4];    /* fresh schedules: each link present w.p. keep/256; schedule i uses level i % 4 */
+  int32_t value_range;      /* initial values uniform in {1..value_range} (BenOr: {0, 1}) */
+  uint32_t redraw_p256;     /* a mutant redraws each initial value w.p. redraw/256 */
+} psg_population_params;
+
+/* Fresh random population over [inst_begin, inst_begin+count) (count <= batch_capacity);
+ * afterwards the range is loaded exactly as by psg_load_schedule + psg_load_inputs. */
+int psg_population_fresh(psg_ctx* ctx, uint64_t inst_begin, uint64_t count, const psg_population_params* p);
+/* Next generation, in place over the loaded population: slot i becomes op[i] == 0 a copy of
+ * slot parent[i], 1 a mutant of slot parent[i] (flips + redraws, then repair), 2 a fresh
+ * schedule (count entries each; parents index the current population). */
+int psg_population_next(psg_ctx* ctx, const uint32_t* parent, const uint8_t* op, const psg_population_params* p);
+/* Copy slots rows[0..k) of the loaded population to the host: ho [k][R][n][W], init [k][n] (nullable). */
+int psg_population_read(psg_ctx* ctx, const uint32_t* rows, size_t k, uint64_t* ho, int32_t* init);
+
 const char* psg_last_error(const psg_ctx* ctx);
 void psg_destroy(psg_ctx* ctx);
 

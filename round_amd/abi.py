@@ -200,3 +200,17 @@ class SpecProgram(C.Structure):
         ("n_vars", C.c_int32),
         ("module_path", C.c_char_p),
     ]
+
+
+class PopulationParams(C.Structure):
+    """psg_population_params (include/psg.h): device-side search populations."""
+    _fields_ = [
+        ("seed", C.c_uint64),
+        ("generation", C.c_uint32),
+        ("flips", C.c_uint32),
+        ("min_size", C.c_int32),
+        ("self_bit", C.c_uint32),
+        ("keep_p256", C.c_uint32 * 4),
+        ("value_range", C.c_int32),
+        ("redraw_p256", C.c_uint32),
+    ]

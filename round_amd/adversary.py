@@ -158,7 +158,7 @@ class Adversary:
                  targets: Optional[Sequence[str]] = None, model: Optional[Model] = None,
                  population: int = 4096, values: int = 3, keep: float = 0.75, self_bit: bool = True,
                  live_rounds: int = 2, live_at: Optional[Sequence[int]] = None, seed: int = 1,
-                 evaluator: Optional[Callable] = None, device: int = 0):
+                 evaluator: Optional[Callable] = None, device: int = 0, device_pop: bool = True):
         if mode not in ("safety", "liveness"):
             raise ValueError("mode must be 'safety' or 'liveness'")
         self.alg, self.n, self.R = alg, n, rounds
@@ -178,6 +178,7 @@ class Adversary:
         self.population, self.values, self.keep = population, values, keep
         self.self_bit, self.live_rounds = self_bit, live_rounds
         self.live_at = None if live_at is None else list(live_at)
+        self.device_pop = device_pop
         self.rng = np.random.default_rng(seed)
         self._own = evaluator is None
         self.evaluator = evaluator or GpuEvaluator(alg, n, rounds, population, device=device,
@@ -291,17 +292,92 @@ class Adversary:
             spread = np.where(decided.any(1), (hi - lo) / max(self.alg.epsilon, 1e-300), 0.0)
             distinct = np.minimum(spread, 10.0)
         else:
-            d = np.where(decided, dec, np.iinfo(np.int32).min)
-            s = np.sort(d, 1)
-            distinct = ((np.diff(s, axis=1) != 0) & (s[:, 1:] != np.iinfo(np.int32).min)).sum(1)
+            lo = np.where(decided, dec, np.iinfo(np.int32).max).min(1)
+            hi = np.where(decided, dec, np.iinfo(np.int32).min).max(1)
+            distinct = (decided.any(1) & (hi != lo)).astype(np.int64)
+            multi = np.nonzero(distinct)[0]
+            if len(multi):  # exact count only where decisions differ (rare)
+                d = np.where(decided[multi], dec[multi], np.iinfo(np.int32).min)
+                srt = np.sort(d, 1)
+                distinct[multi] = ((np.diff(srt, axis=1) != 0) & (srt[:, 1:] != np.iinfo(np.int32).min)).sum(1)
         if self.mode == "liveness":
             late = ev.summary["term_round"].astype(np.float64)
             return late + 0.1 * (~decided).sum(1) + self.rng.random(len(late)) * 1e-3
         return 4.0 * distinct + failed.sum(1) + 0.05 * decided.sum(1) / self.n + self.rng.random(len(ff)) * 1e-3
 
     # -------------------------------------------------------------- search
+    def device_population(self) -> bool:
+        """Can generations be generated and mutated on the GPU (psg_population_*)?
+        General omission, safety search, integer inputs, the GPU evaluator."""
+        return (self.model.family == "omission" and self.mode == "safety" and not self.alg.real
+                and isinstance(self.evaluator, GpuEvaluator) and self.device_pop)
+
+    def _pop_params(self, generation):
+        p = abi.PopulationParams()
+        p.seed = int(self.rng.integers(0, 1 << 63)) if generation == 0 else self._pop_seed
+        if generation == 0:
+            self._pop_seed = p.seed
+        p.generation = generation
+        p.flips = max(1, int(self.n * self.R * 0.01))
+        p.min_size = self.model.min_size or 0
+        p.self_bit = 1 if self.self_bit else 0
+        for j, f in enumerate((0.7, 0.85, 1.0, 1.15)):  # the host generator's spread of loss rates
+            p.keep_p256[j] = int(round(min(0.97, self.keep * f) * 256))
+        p.value_range = self.values
+        p.redraw_p256 = 5  # ~2 % of a mutant's initial values redrawn
+        return p
+
+    def _search_device(self, generations, want, time_budget, elite_frac, fresh_frac, shrink):
+        """The search loop with the population resident in HBM: per generation one
+        psg_run_batch, the per-instance summaries + decisions to the host for scoring,
+        and psg_population_next with the chosen parents (no HO set crosses PCIe)."""
+        P = self.population
+        ctx = self.evaluator.gr._ctx
+        base = self.next_id
+        self.next_id += P
+        ctx.population_fresh(base, P, self._pop_params(0))
+        found: List[Counterexample] = []
+        t0 = time.perf_counter()
+        gpu = 0.0
+        history = []
+        g = 0
+        for g in range(1, generations + 1):
+            t1 = time.perf_counter()
+            _, pi = ctx.run_batch_np(base, P)
+            dec, dr = ctx.copy_decisions_np()
+            gpu += time.perf_counter() - t1
+            ev = Eval(pi, dec, dr)
+            bad, first = self._violations(ev)
+            rows = np.nonzero(bad)[0][:max(0, want - len(found))]
+            if len(rows):
+                hos, inits = ctx.population_read(rows)
+                for j, i in enumerate(rows):
+                    found.append(self._cex(base + int(i), inits[j], hos[j], None, pi[i], int(first[i])))
+            score = self._score(ev)
+            history.append(float(score.max()))
+            if len(found) >= want or (time_budget is not None and time.perf_counter() - t0 > time_budget):
+                break
+            order = np.argsort(-score)
+            ne = max(1, int(P * elite_frac))
+            nf = int(P * fresh_frac)
+            nm = P - ne - nf
+            elite = order[:ne]
+            parent = np.zeros(P, np.uint32)
+            op = np.full(P, 2, np.uint8)
+            parent[:ne], op[:ne] = elite, 0
+            parent[ne:ne + nm], op[ne:ne + nm] = elite[self.rng.integers(0, ne, nm)], 1
+            t1 = time.perf_counter()
+            ctx.population_next(parent, op, self._pop_params(g))
+            gpu += time.perf_counter() - t1
+        secs = time.perf_counter() - t0
+        if shrink:
+            found = [self.shrink(c) for c in found]
+        return SearchResult(found, P * g, g, secs, gpu, history)
+
     def search(self, generations: int = 50, want: int = 1, time_budget: Optional[float] = None,
                elite_frac: float = 0.25, fresh_frac: float = 0.25, shrink: bool = True) -> SearchResult:
+        if self.device_population():
+            return self._search_device(generations, want, time_budget, elite_frac, fresh_frac, shrink)
         P = self.population
         genome = self._fresh(P)
         init = default_init(self.alg, self.rng, P, self.n, self.values)

@@ -72,6 +72,12 @@ struct psg_ctx {
   uint64_t ho_cap = 0;  // instances d_ho / d_crash hold
   bool ho_loaded = false, ho_has_crash = false;
   uint64_t ho_begin = 0, ho_count = 0;
+  // search populations (psg_population_*): second buffers of the HO sets / inputs
+  uint64_t* d_ho2 = nullptr;
+  int32_t* d_init2 = nullptr;
+  uint32_t* d_parent = nullptr;
+  uint8_t* d_op = nullptr;
+  uint64_t pop_cap = 0;
   int32_t* d_dec = nullptr;
   uint8_t* d_dround = nullptr;
   psg_instance_summary* d_inst = nullptr;
@@ -872,6 +878,134 @@ int psg_materialize_schedule(psg_ctx* c, uint64_t inst_begin, uint64_t count, ui
   return rc;
 }
 
+// ---------------------------------------------------------------- search populations
+static int pop_buffers(psg_ctx* c, uint64_t count) {
+  const uint64_t n = (uint64_t)c->cfg.n, R = (uint64_t)c->cfg.rounds, W = (uint64_t)c->W;
+  if (count > c->ho_cap) {  // the loaded-schedule buffers (psg_load_schedule's)
+    if (c->d_ho) (void)hipFree(c->d_ho);
+    if (c->d_crash) (void)hipFree(c->d_crash);
+    c->d_ho = nullptr;
+    c->d_crash = nullptr;
+    c->ho_cap = 0;
+    c->ho_loaded = false;
+    HIPCHK(c, hipMalloc(&c->d_ho, sizeof(uint64_t) * count * R * n * W));
+    HIPCHK(c, hipMalloc(&c->d_crash, sizeof(int32_t) * count * n));
+    c->ho_cap = count;
+  }
+  if (count > c->pop_cap) {
+    if (c->d_ho2) (void)hipFree(c->d_ho2);
+    if (c->d_init2) (void)hipFree(c->d_init2);
+    if (c->d_parent) (void)hipFree(c->d_parent);
+    if (c->d_op) (void)hipFree(c->d_op);
+    c->d_ho2 = nullptr;
+    c->d_init2 = nullptr;
+    c->d_parent = nullptr;
+    c->d_op = nullptr;
+    c->pop_cap = 0;
+    const uint64_t cap = std::max(count, c->ho_cap);
+    HIPCHK(c, hipMalloc(&c->d_ho2, sizeof(uint64_t) * cap * R * n * W));
+    HIPCHK(c, hipMalloc(&c->d_init2, sizeof(int32_t) * c->cap * n));
+    HIPCHK(c, hipMalloc(&c->d_parent, sizeof(uint32_t) * cap));
+    HIPCHK(c, hipMalloc(&c->d_op, cap));
+    c->pop_cap = cap;
+  }
+  return PSG_OK;
+}
+
+static int pop_check(psg_ctx* c, const psg_population_params* p) {
+  if (!p) return fail(c, PSG_EINVAL, "null population parameters");
+  if (c->cfg.alg == PSG_ALG_EPSILON) return fail(c, PSG_EINVAL, "populations hold int32 inputs (not EpsilonConsensus)");
+  if (c->cfg.alg != PSG_ALG_BENOR && p->value_range < 1) return fail(c, PSG_EINVAL, "value_range must be >= 1");
+  if (p->min_size > c->cfg.n) return fail(c, PSG_EINVAL, "min_size > n");
+  return PSG_OK;
+}
+
+static PopArgs pop_args(const psg_ctx* c, const psg_population_params* p, uint64_t count) {
+  PopArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.count = count;
+  a.n = c->cfg.n;
+  a.R = c->cfg.rounds;
+  a.W = c->W;
+  a.seed = p->seed;
+  a.gen = p->generation;
+  a.flips = p->flips;
+  a.min_size = p->min_size;
+  a.self_bit = p->self_bit;
+  for (int j = 0; j < 4; ++j) a.keep[j] = p->keep_p256[j];
+  a.V = p->value_range;
+  a.redraw = p->redraw_p256;
+  a.benor = c->cfg.alg == PSG_ALG_BENOR;
+  return a;
+}
+
+int psg_population_fresh(psg_ctx* c, uint64_t inst_begin, uint64_t count, const psg_population_params* p) {
+  if (!c) return PSG_EINVAL;
+  if (int rc = pop_check(c, p)) return rc;
+  if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (int rc = pop_buffers(c, std::max<uint64_t>(count, 1))) return rc;
+  PopArgs a = pop_args(c, p, count);
+  a.ho = c->d_ho;
+  a.init = c->d_init;
+  HIPCHK(c, launch_population(a, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->ho_loaded = true;
+  c->ho_has_crash = false;
+  c->ho_begin = inst_begin;
+  c->ho_count = count;
+  c->staged = true;
+  c->staged_begin = inst_begin;
+  c->staged_count = count;
+  return PSG_OK;
+}
+
+int psg_population_next(psg_ctx* c, const uint32_t* parent, const uint8_t* op, const psg_population_params* p) {
+  if (!c) return PSG_EINVAL;
+  if (int rc = pop_check(c, p)) return rc;
+  if (!(c->ho_loaded && c->staged && c->staged_begin == c->ho_begin && c->staged_count == c->ho_count) ||
+      c->pop_cap < c->ho_count)
+    return fail(c, PSG_EINVAL, "no population loaded (psg_population_fresh first)");
+  const uint64_t count = c->ho_count;
+  if (count && (!parent || !op)) return fail(c, PSG_EINVAL, "null parent / op");
+  for (uint64_t i = 0; i < count; ++i) {
+    if (op[i] > 2) return fail(c, PSG_EINVAL, "op must be 0 (copy), 1 (mutate) or 2 (fresh)");
+    if (op[i] != 2 && parent[i] >= count) return fail(c, PSG_ERANGE, "parent index outside the population");
+  }
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, hipMemcpyAsync(c->d_parent, parent, sizeof(uint32_t) * count, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_op, op, count, hipMemcpyHostToDevice, c->stream));
+  PopArgs a = pop_args(c, p, count);
+  a.src = c->d_ho;
+  a.ho = c->d_ho2;
+  a.src_init = c->d_init;
+  a.init = c->d_init2;
+  a.parent = c->d_parent;
+  a.op = c->d_op;
+  HIPCHK(c, launch_population(a, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::swap(c->d_ho, c->d_ho2);  // the new generation is the loaded schedule / staged inputs
+  std::swap(c->d_init, c->d_init2);
+  std::swap(c->ho_cap, c->pop_cap);
+  c->pop_cap = std::min(c->pop_cap, c->ho_cap);
+  return PSG_OK;
+}
+
+int psg_population_read(psg_ctx* c, const uint32_t* rows, size_t k, uint64_t* ho, int32_t* init) {
+  if (!c || (!rows && k) || (!ho && k)) return PSG_EINVAL;
+  if (!c->ho_loaded) return fail(c, PSG_EINVAL, "no population loaded");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const uint64_t n = (uint64_t)c->cfg.n, R = (uint64_t)c->cfg.rounds, W = (uint64_t)c->W;
+  for (size_t j = 0; j < k; ++j) {
+    if (rows[j] >= c->ho_count) return fail(c, PSG_ERANGE, "row outside the population");
+    HIPCHK(c, hipMemcpy(ho + j * R * n * W, c->d_ho + (uint64_t)rows[j] * R * n * W, sizeof(uint64_t) * R * n * W,
+                        hipMemcpyDeviceToHost));
+    if (init && c->staged)
+      HIPCHK(c, hipMemcpy(init + j * n, c->d_init + (uint64_t)rows[j] * n, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  }
+  return PSG_OK;
+}
+
 const char* psg_last_error(const psg_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
 
 void psg_destroy(psg_ctx* c) {
@@ -894,6 +1028,10 @@ void psg_destroy(psg_ctx* c) {
   if (c->d_prog) (void)hipFree(c->d_prog);
   if (c->d_ho) (void)hipFree(c->d_ho);
   if (c->d_crash) (void)hipFree(c->d_crash);
+  if (c->d_ho2) (void)hipFree(c->d_ho2);
+  if (c->d_init2) (void)hipFree(c->d_init2);
+  if (c->d_parent) (void)hipFree(c->d_parent);
+  if (c->d_op) (void)hipFree(c->d_op);
   if (c->module) (void)hipModuleUnload(c->module);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);

@@ -66,6 +66,26 @@ struct VmArgs {
   int32_t* err;                  // OR of VM_ERR_* over all instances
 };
 
+// Search-population kernels (psg_population.hip)
+struct PopArgs {
+  uint64_t* ho;             // destination population [count][R][n][W]
+  const uint64_t* src;      // current population (next generation), null for fresh
+  int32_t* init;            // destination initial values [count][n]
+  const int32_t* src_init;  // current initial values
+  const uint32_t* parent;   // [count] (null for fresh)
+  const uint8_t* op;        // [count] 0 copy, 1 mutate, 2 fresh (null: all fresh)
+  uint64_t count;
+  int n, R, W;
+  uint64_t seed;
+  uint32_t gen, flips;
+  int32_t min_size;
+  uint32_t self_bit;
+  uint32_t keep[4];
+  int32_t V;
+  uint32_t redraw;
+  int benor;
+};
+
 // global counter layout (uint64 each)
 enum { C_FAIL = 0, C_DECIDED = PSG_MAX_CHECKS, C_DIGEST = PSG_MAX_CHECKS + 1, C_HIST = PSG_MAX_CHECKS + 2,
        NCOUNTERS = C_HIST + PSG_MAX_ROUNDS + 2 };

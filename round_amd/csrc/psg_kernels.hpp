@@ -5,6 +5,7 @@
 namespace psg {
 struct KArgs;
 struct VmArgs;
+struct PopArgs;
 
 hipError_t launch_otr(const KArgs& a, int W, int grid, hipStream_t s);
 hipError_t launch_lv(const KArgs& a, int W, int grid, hipStream_t s);
@@ -28,6 +29,7 @@ const void* epsilon_kernel_ptr(int W);
 
 hipError_t launch_champ_selftest(const uint64_t* sets, int count, int tiebreak, int32_t* out, hipStream_t s);
 hipError_t launch_schedule(const KArgs& a, int W, int grid, uint64_t* ho_out, int32_t* crash_out, hipStream_t s);
+hipError_t launch_population(const PopArgs& a, hipStream_t s);
 hipError_t launch_spec_vm(const VmArgs& a, int grid, hipStream_t s);
 hipError_t launch_gen_init(uint64_t inst_begin, uint64_t count, int n, int alg, int V, uint64_t seed, int32_t* out,
                            hipStream_t s);

@@ -24,6 +24,7 @@ EXPORTED_SYMBOLS = [
     "psg_fetch_instances", "psg_last_error", "psg_destroy", "psg_create_error",
     "psg_selftest_map_head", "psg_load_inputs_f64", "psg_copy_decisions_f64", "psg_fetch_instances_f64",
     "psg_run_batch_spec", "psg_load_schedule", "psg_clear_schedule", "psg_materialize_schedule",
+    "psg_population_fresh", "psg_population_next", "psg_population_read",
 ]
 
 
@@ -71,6 +72,9 @@ def load():
     L.psg_load_schedule.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]
     L.psg_clear_schedule.argtypes = [C.c_void_p]
     L.psg_materialize_schedule.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]
+    L.psg_population_fresh.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(abi.PopulationParams)]
+    L.psg_population_next.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(abi.PopulationParams)]
+    L.psg_population_read.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
     L.psg_selftest_map_head.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
                                         C.POINTER(C.c_int32)]
     _lib = L
@@ -236,6 +240,32 @@ class Context:
         self._check(load().psg_materialize_schedule(self._h, inst_begin, count, ho.ctypes.data_as(C.c_void_p),
                                                     cr.ctypes.data_as(C.c_void_p)))
         return ho, cr
+
+    def population_fresh(self, inst_begin, count, params):
+        """psg_population_fresh: a random population of explicit schedules + inputs, on the device."""
+        self._check(load().psg_population_fresh(self._h, inst_begin, count, C.byref(params)))
+
+    def population_next(self, parent, op, params):
+        """psg_population_next: slot i <- copy (op 0) / mutant (1) of slot parent[i], or fresh (2)."""
+        import numpy as np
+        parent = np.ascontiguousarray(parent, np.uint32)
+        op = np.ascontiguousarray(op, np.uint8)
+        if parent.shape != op.shape:
+            raise ValueError("parent and op must have one entry per slot")
+        self._check(load().psg_population_next(self._h, parent.ctypes.data_as(C.c_void_p),
+                                               op.ctypes.data_as(C.c_void_p), C.byref(params)))
+
+    def population_read(self, rows):
+        """Slots `rows` of the loaded population: (ho uint64 [k][R][n][W], init int32 [k][n])."""
+        import numpy as np
+        rows = np.ascontiguousarray(rows, np.uint32)
+        k = int(rows.shape[0])
+        W = (self.cfg.n + 63) // 64
+        ho = np.zeros((k, self.cfg.rounds, self.cfg.n, W), np.uint64)
+        init = np.zeros((k, self.cfg.n), np.int32)
+        self._check(load().psg_population_read(self._h, rows.ctypes.data_as(C.c_void_p), k,
+                                               ho.ctypes.data_as(C.c_void_p), init.ctypes.data_as(C.c_void_p)))
+        return ho, init
 
     def close(self):
         if getattr(self, "_h", None):

@@ -48,6 +48,8 @@ int main(void) {
   P(psg_summary, fail_count) P(psg_summary, decided_processes) P(psg_summary, term_hist) P(psg_summary, kernel_ns)
   P(psg_instance_summary, first_fail) P(psg_instance_summary, term_round) P(psg_instance_summary, n_decided)
   P(psg_schedule, crash_fmax) P(psg_schedule, self_bit)
+  printf("psg_population_params %zu\n", sizeof(psg_population_params));
+  P(psg_population_params, flips) P(psg_population_params, keep_p256) P(psg_population_params, redraw_p256)
   return 0;
 }
 """
@@ -80,6 +82,10 @@ def test_struct_layouts_match_header(tmp_path):
         "psg_instance_summary.n_decided": abi.InstanceSummary.n_decided.offset,
         "psg_schedule.crash_fmax": abi.Schedule.crash_fmax.offset,
         "psg_schedule.self_bit": abi.Schedule.self_bit.offset,
+        "psg_population_params": C.sizeof(abi.PopulationParams),
+        "psg_population_params.flips": abi.PopulationParams.flips.offset,
+        "psg_population_params.keep_p256": abi.PopulationParams.keep_p256.offset,
+        "psg_population_params.redraw_p256": abi.PopulationParams.redraw_p256.offset,
     }
     assert {k: int(v) for k, v in got.items()} == want
 

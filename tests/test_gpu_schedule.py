@@ -227,3 +227,99 @@ def test_adversary_liveness_otr_two_good_rounds():
     with A.Adversary(psync.OTR(), n, R, mode="liveness", live_at=[0, 1], population=2048, seed=14) as adv:
         res = adv.search(generations=5, want=1, shrink=False)
     assert not res.counterexamples
+
+
+# ---------------------------------------------------------------- device-resident search populations
+
+def _pop_params(seed=5, gen=0, flips=6, min_size=0, self_bit=1, keep=(128, 192, 224, 256), V=3, redraw=5):
+    p = abi.PopulationParams()
+    p.seed, p.generation, p.flips, p.min_size, p.self_bit = seed, gen, flips, min_size, self_bit
+    for j, k in enumerate(keep):
+        p.keep_p256[j] = k
+    p.value_range, p.redraw_p256 = V, redraw
+    return p
+
+
+def _bits(ho, n):
+    return np.unpackbits(ho.view(np.uint8), bitorder="little").reshape(ho.shape[:-1] + (-1,))[..., :n]
+
+
+@pytest.mark.parametrize("alg,n", [(psync.OTR(), 64), (psync.BenOr(), 70)], ids=["otr-n64", "benor-n70"])
+def test_population_fresh_properties(alg, n):
+    P, R = 400, 6
+    min_size = n // 2 + 1 if alg.alg_id == abi.PSG_ALG_BENOR else 0
+    with psync.GpuRound(alg, n, R, batch_capacity=P) as g:
+        g._ctx.population_fresh(10, P, _pop_params(min_size=min_size))
+        ho, init = g._ctx.population_read(np.arange(P))
+    b = _bits(ho, n)
+    assert (b[:, :, np.arange(n), np.arange(n)] == 1).all()                 # self bit
+    W = (n + 63) // 64
+    tail = _bits(ho, 64 * W)[..., n:]
+    assert not tail.any()                                                  # no pid >= n
+    sizes = b.sum(-1)
+    assert (sizes >= min_size).all()
+    assert (sizes[3::4] == n).all()                                        # keep 256/256: everyone
+    if min_size == 0:
+        off = b[0::4].sum() - P // 4 * R * n                               # keep 128/256, self bits aside
+        assert abs(off / (P // 4 * R * n * (n - 1)) - 0.5) < 0.02
+    if alg.alg_id == abi.PSG_ALG_BENOR:
+        assert set(np.unique(init)) <= {0, 1}
+    else:
+        assert init.min() >= 1 and init.max() <= 3 and len(np.unique(init)) == 3
+
+
+def test_population_next_ops_and_determinism(oracle_mod):
+    n, R, P = 32, 5, 64
+    flips = 7
+    outs = []
+    for _ in range(2):  # same parameters -> same populations (a pure function of them)
+        with psync.GpuRound(psync.OTR(), n, R, batch_capacity=P, value_range=3) as g:
+            ctx = g._ctx
+            ctx.population_fresh(0, P, _pop_params(flips=flips))
+            ho0, in0 = ctx.population_read(np.arange(P))
+            parent = np.array([5] * 10 + [3] * 30 + [0] * (P - 40), np.uint32)
+            op = np.array([0] * 10 + [1] * 30 + [2] * (P - 40), np.uint8)
+            ctx.population_next(parent, op, _pop_params(gen=1, flips=flips))
+            ho1, in1 = ctx.population_read(np.arange(P))
+            _, pi = ctx.run_batch_np(0, P)
+        outs.append((ho0, in0, ho1, in1, pi))
+        # copies are exact, mutants differ from the parent in at most `flips` links
+        assert (ho1[:10] == ho0[5]).all() and (in1[:10] == in0[5]).all()
+        diff = (_bits(ho1[10:40], n) != _bits(ho0[3][None], n)).sum((1, 2, 3))
+        assert (diff <= flips).all() and (diff > 0).any()
+        assert (in1[10:40] != in0[3]).mean() < 0.2
+        assert (_bits(ho1, n)[:, :, np.arange(n), np.arange(n)] == 1).all()
+        # the kernels run exactly the loaded population (oracle under the read-back sets)
+        _, opi, _, _, _ = oracle_mod.run_schedule(g.cfg, 0, P, ho1, None, in1, per_instance=True)
+        assert [int(x["digest"]) for x in pi] == [x.digest for x in opi]
+    a, b = outs
+    assert all((x == y).all() for x, y in zip(a[:4], b[:4]))
+
+
+def test_population_argument_errors():
+    with psync.GpuRound(psync.OTR(), 16, 4, batch_capacity=8) as g:
+        ctx = g._ctx
+        with pytest.raises(lib.PsgError):
+            ctx.population_next(np.zeros(8, np.uint32), np.zeros(8, np.uint8), _pop_params())  # nothing loaded
+        ctx.population_fresh(0, 8, _pop_params())
+        with pytest.raises(lib.PsgError):
+            ctx.population_next(np.full(8, 9, np.uint32), np.ones(8, np.uint8), _pop_params())  # parent >= 8
+        with pytest.raises(lib.PsgError):
+            ctx.population_next(np.zeros(8, np.uint32), np.full(8, 3, np.uint8), _pop_params())  # bad op
+        with pytest.raises(lib.PsgError):
+            ctx.population_fresh(0, 9, _pop_params())  # > batch_capacity
+        with pytest.raises(lib.PsgError):
+            ctx.population_read(np.array([8], np.uint32))
+    with psync.GpuRound(psync.EpsilonConsensus(), 8, 4, batch_capacity=8) as g:
+        with pytest.raises(lib.PsgError):
+            g._ctx.population_fresh(0, 8, _pop_params())
+
+
+def test_device_and_host_search_paths_agree_on_outcome():
+    """The device-population search and the host one both find the OTR mutant."""
+    for dp in (True, False):
+        with A.Adversary(psync.OTR(variant=1), 16, 8, targets=["Agreement"], population=2048, values=2, seed=3,
+                         device_pop=dp) as adv:
+            assert adv.device_population() == dp
+            res = adv.search(generations=40, want=1)
+        assert res.counterexamples and res.counterexamples[0].violated == ["Agreement"]
