@@ -204,13 +204,16 @@ static int run_kernel(psg_ctx* c, KArgs& a, uint64_t count, psg_summary* out, bo
   uint64_t want = (count + G - 1) / G;
   int grid = (int)std::min<uint64_t>(want, (uint64_t)c->grid_max);
   if (grid < 1) grid = 1;
-  HIPCHK(c, hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long) * NCOUNTERS, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long) * NCOUNTERS_ALLOC, c->stream));
   if (timed) HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   HIPCHK(c, launch_alg(c, a, grid));
   if (timed) HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-  unsigned long long host[NCOUNTERS];
+  unsigned long long host[NCOUNTERS_ALLOC];
   HIPCHK(c, hipMemcpyAsync(host, c->d_counters, sizeof(host), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (PSG_PHASE_TIMERS && std::getenv("PSG_PHASE_TIMERS"))  // profiling builds: cycles per phase
+    std::fprintf(stderr, "psg phase cycles: setup %llu active %llu check_only %llu finish %llu\n", host[C_TIMER],
+                 host[C_TIMER + 1], host[C_TIMER + 2], host[C_TIMER + 3]);
   if (out) {
     std::memset(out, 0, sizeof(*out));
     out->instances = (int64_t)count;
@@ -426,7 +429,7 @@ int psg_create(psg_ctx** out, const psg_config* cfg) {
   CK(hipMalloc(&c->d_dec, sizeof(int32_t) * cells));
   CK(hipMalloc(&c->d_dround, sizeof(uint8_t) * cells));
   CK(hipMalloc(&c->d_inst, sizeof(psg_instance_summary) * c->cap));
-  CK(hipMalloc(&c->d_counters, sizeof(unsigned long long) * NCOUNTERS));
+  CK(hipMalloc(&c->d_counters, sizeof(unsigned long long) * NCOUNTERS_ALLOC));
   const void* kp = kernel_ptr(cfg->alg, c->W);
   int per_cu = 0;
   const int threads = c->W == 1 ? 256 : 64 * c->W;

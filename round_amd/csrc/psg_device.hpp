@@ -88,7 +88,37 @@ struct PopArgs {
 
 // global counter layout (uint64 each)
 enum { C_FAIL = 0, C_DECIDED = PSG_MAX_CHECKS, C_DIGEST = PSG_MAX_CHECKS + 1, C_HIST = PSG_MAX_CHECKS + 2,
-       NCOUNTERS = C_HIST + PSG_MAX_ROUNDS + 2 };
+       NCOUNTERS = C_HIST + PSG_MAX_ROUNDS + 2,
+       // profiling builds only (-DPSG_PHASE_TIMERS=1): per-phase shader cycles summed over waves
+       C_TIMER = NCOUNTERS, NTIMERS = 4, NCOUNTERS_ALLOC = NCOUNTERS + NTIMERS };
+
+#ifndef PSG_PHASE_TIMERS
+#define PSG_PHASE_TIMERS 0
+#endif
+// Phase timers of a profiling build: t.mark(j) charges the cycles since the last
+// mark to phase j (uniform, kept in SGPRs); flush adds them to the global slots.
+struct PhaseTimers {
+#if PSG_PHASE_TIMERS
+  uint64_t last, acc[NTIMERS];
+  PSG_DEV void start() {
+    for (int j = 0; j < NTIMERS; ++j) acc[j] = 0;
+    last = __builtin_amdgcn_s_memtime();
+  }
+  PSG_DEV void mark(int j) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    acc[j] += t - last;
+    last = t;
+  }
+  PSG_DEV void flush(unsigned long long* g, int lane) {
+    if (lane == 0)
+      for (int j = 0; j < NTIMERS; ++j) atomicAdd(&g[C_TIMER + j], (unsigned long long)acc[j]);
+  }
+#else
+  PSG_DEV void start() {}
+  PSG_DEV void mark(int) {}
+  PSG_DEV void flush(unsigned long long*, int) {}
+#endif
+};
 
 constexpr uint32_t ROUND_INIT = 0xFFFFFFFFu;
 constexpr uint32_t ROUND_CRASH = 0xFFFFFFFEu;

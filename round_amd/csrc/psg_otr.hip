@@ -84,6 +84,8 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
   const Mask<W> full = mfull<W>(n);
   const uint32_t valid01 = g.valid ? 1u : 0u;
 
+  PhaseTimers pt;  // profiling builds only
+  pt.start();
   for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;
@@ -105,6 +107,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
       trace_put<W>(g, a, i, c, x, (int32_t)dec01, V2 && !dec01 ? PSG_NONE32 : decision, 0, 0, 0, 0, 0, hs);
     };
     if (a.trace) trace(0, n);
+    pt.mark(0);
 
     for (int k = 0; k < a.R; ++k) {
       const uint32_t old01 = dec01;
@@ -160,9 +163,12 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
       }
       otr_check<W, V2>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, old01, old_decision, valid01);
       if (a.trace) trace(k + 1, hs);
+      pt.mark(many(act) ? 1 : 2);
     }
     finish_instance<W>(g, a, i, ck, 8, dec_val, dec_round, halt_round, x, &bc);
+    pt.mark(3);
   }
+  pt.flush(a.counters, threadIdx.x & 63);
   __syncthreads();
   counters_flush(&bc, a.counters, 8, a.R);
 }
