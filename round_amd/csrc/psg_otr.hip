@@ -23,13 +23,15 @@ struct OtrLds {
 
 // Spec check at check point c (spec r = c). Slots: 0 Safety (some invariant
 // holds), 1..3 invariants, 4 Agreement, 5 Validity, 6 Integrity, 7 Irrevocability.
-// Every formula is evaluated from scratch at every check point. The per-process
-// parts of the universally quantified formulas are computed as 0/1 VALU words and
-// OR-reduced over the wave in one DPP pass:
-//   bit 0  !(i.x == init(j.x) for some j)           keepInit   (X0-set probe)
-//   bit 1  i.decided && i.decision != d0            Agreement  (d0 = a decided value)
-//   bit 2  i.decided && i.decision not initial      Validity
-//   bit 3  old(i.decided) && !(i.decided && old(i.decision) == i.decision)  Irrevocability
+// Every formula is evaluated from scratch at every check point. Each universally
+// quantified part is one ballot of its per-process witness:
+//   !(i.x == init(j.x) for some j)                  keepInit   (X0-set probe)
+//   i.decided && i.decision != d0                   Agreement  (d0 = a decided value)
+//   i.decided && i.decision not initial             Validity
+//   old(i.decided) && !(i.decided && old(i.decision) == i.decision)  Irrevocability
+// (Packing the witnesses into one word and OR-reducing it with a DPP pass was
+// measured 28 % slower on the headline launch: the DPP chain's latency outweighs
+// the scalar mask work it removes, profiles/s2_ab/ab5.log.)
 // V.exists(v => |{i : i.x == v}| > 2n/3 && all decisions == v): with decisions only
 // v = d0 can qualify; without, v must be a strict majority (Boyer-Moore candidate).
 template <int W, bool V2>
