@@ -34,6 +34,9 @@ struct Ctx {
   int32_t i[PSG_NFIELDS];
   int32_t* sc;             // W > 1: staged copies [3][PSG_NFIELDS][64W]
   X0Set<W> iset[2];        // membership sets of init(field) values (S::kInitSet0 / kInitSet1)
+  // per check point: majority candidates already computed (key field | tag << 8, -1 = empty);
+  // scalar slots, not an array, so they stay in registers
+  int32_t maj_k0, maj_v0, maj_k1, maj_v1;
   PSG_DEV const int32_t* stage(int tag, int f) const { return sc + (tag * PSG_NFIELDS + f) * 64 * W; }
   PSG_DEV int32_t own(int tag, int f) const { return tag == PSG_TAG_CUR ? c[f] : (tag == PSG_TAG_OLD ? o[f] : i[f]); }
 };
@@ -270,10 +273,25 @@ PSG_DEV int32_t exists_int_eq(Ctx<W>& x, const int32_t (&ev)[NE > 0 ? NE : 1],
 // a value of the per-process term t held by at least L processes. With 2L > n
 // that is the strict majority (Boyer-Moore candidate, one body evaluation);
 // otherwise the distinct values of t filtered by their count. Requires L >= 1.
-template <int W, class Fn>
+template <int W, int KEY, class Fn>
 PSG_DEV int32_t exists_int_guard(Ctx<W>& x, int32_t t, const int32_t* staged, int32_t L, Fn fn) {
   if (2 * (int64_t)L > (int64_t)x.n) {
-    const int32_t m = majority_candidate<W>(x.g, t);
+    // the candidate depends only on the field's values: computed once per check point
+    int32_t m;
+    if (x.maj_k0 == KEY) {
+      m = x.maj_v0;
+    } else if (x.maj_k1 == KEY) {
+      m = x.maj_v1;
+    } else {
+      m = majority_candidate<W>(x.g, t);
+      if (x.maj_k0 < 0) {
+        x.maj_k0 = KEY;
+        x.maj_v0 = m;
+      } else if (x.maj_k1 < 0) {
+        x.maj_k1 = KEY;
+        x.maj_v1 = m;
+      }
+    }
     if (mpopc(x.g.ballot(t == m)) < L) return 0;
     return fn(m) != 0 ? 1 : 0;
   }
@@ -339,7 +357,21 @@ __device__ void native_kernel_body(const VmArgs& A) {
     ck.reset();
     for (int c = 0; c <= A.R; ++c) {
       x.r = c;
-      if (S::kTags & 2u) load(x.o, base + (uint64_t)(c > 0 ? c - 1 : 0) * rowsz, PSG_TAG_OLD);
+      x.maj_k0 = x.maj_k1 = -1;
+      if (S::kTags & 2u) {
+        // old = the previous check point's current state, already in registers
+        // (c = 0: the initial state, read below); halves the trace read traffic
+        if (c == 0) {
+          load(x.o, base, PSG_TAG_OLD);
+        } else {
+#pragma unroll
+          for (int f = 0; f < PSG_NFIELDS; ++f) {
+            if (!((S::kFields >> f) & 1u)) continue;
+            x.o[f] = x.c[f];
+            if constexpr (W > 1) stg[(PSG_TAG_OLD * PSG_NFIELDS + f) * 64 * W + g.pid] = x.c[f];
+          }
+        }
+      }
       load(x.c, base + (uint64_t)c * rowsz, PSG_TAG_CUR);
       if constexpr (W > 1) __syncthreads();
       uint32_t fb = S::template fail<W>(x, scratch[grp]);

@@ -692,9 +692,12 @@ class _Gen:
         self.max_vi = 0
         self.tuples = {}      # var uid -> {(field, tag): C++ name} (serial quantifier over distinct states)
         self.init_sets = []   # fields f with an LDS membership set of init(f) (at most 2)
+        self.cse = {}         # id(closed subformula) -> C++ name of its hoisted value
 
     def gen(self, e, in_lane, vi_depth):
         """(C++ expression, depends on the lane)."""
+        if id(e) in self.cse:
+            return self.cse[id(e)], False  # a closed subformula computed once per check point
         if isinstance(e, Lit):
             return _c_int(e.v), False
         if isinstance(e, NVal):
@@ -809,7 +812,7 @@ class _Gen:
             body, lane = self.gen(q.body, in_lane, vi_depth + 1)
             self.max_vi = max(self.max_vi, vi_depth + 1)
             return (f"([&]() -> int32_t {{ const int32_t L_ = {L}; if (L_ >= 1) return "
-                    f"spec::exists_int_guard<W>(x, x.own({tag}, {f}), x.stage({tag}, {f}), L_, "
+                    f"spec::exists_int_guard<W, {f | (tag << 8)}>(x, x.own({tag}, {f}), x.stage({tag}, {f}), L_, "
                     f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); return {general}; }})()"), True
         return self._vint_general(q, v, in_lane, vi_depth)
 
@@ -922,6 +925,29 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
     invs = [inv if guard is None else (inv & guard) for inv in spec.invariants]
     lines = []
     slot = 0
+    # common closed subformulas (the same Formula object used by several slots, e.g.
+    # OTR's keepInit in Invariant0 and Invariant1): hoisted, evaluated once per check point
+    roots = list(invs) + [f for name, f in spec.properties if name != "Termination"]
+    if spec.safety_predicate is not None:
+        roots.append(spec.safety_predicate)
+    seen, order = {}, []
+
+    def visit(e):
+        seen[id(e)] = seen.get(id(e), 0) + 1
+        if seen[id(e)] > 1:
+            return
+        for c in e.children():
+            visit(c)
+        order.append(e)  # post-order: inner subformulas first
+
+    for rt in roots:
+        visit(rt)
+    for e in order:
+        if seen[id(e)] > 1 and isinstance(e, (Quant, Contains)) and not _free_vars(e):
+            c, _ = gen.gen(e, False, 0)
+            name = f"cse{len(gen.cse)}"
+            lines.append(f"    const int32_t {name} = {c};")
+            gen.cse[id(e)] = name
     if invs:
         for k, inv in enumerate(invs):
             c, _ = gen.gen(inv, False, 0)
