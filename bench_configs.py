@@ -58,6 +58,11 @@ def configs(scale):
                 lambda: formula.compile_native(formula.otr_spec(), abi.PSG_ALG_OTR)))
     out.append(("G1_lv_n64_native", psync.LastVoting(), 64, int(2_500_000 * s), {}, 42,
                 lambda: formula.compile_native(formula.lv_spec(), abi.PSG_ALG_LAST_VOTING)))
+    # ... and fused into the round kernel (one launch, Spec evaluated from registers, no trace)
+    out.append(("G1_otr_n64_fused", psync.OTR(), 64, int(10_000_000 * s), dict(value_range=64), 24,
+                lambda: formula.compile_native(formula.otr_spec(), abi.PSG_ALG_OTR, fused=True, n=64)))
+    out.append(("G1_lv_n64_fused", psync.LastVoting(), 64, int(12_500_000 * s), {}, 42,
+                lambda: formula.compile_native(formula.lv_spec(), abi.PSG_ALG_LAST_VOTING, fused=True, n=64)))
     return out
 
 

@@ -64,6 +64,7 @@ struct psg_ctx {
   std::string module_path;       // native Spec code object currently loaded
   hipModule_t module = nullptr;
   hipFunction_t native_fn = nullptr;
+  hipFunction_t fused_fn = nullptr, fused_x_fn = nullptr;  // fused Spec module: round kernel + Spec
   bool staged = false;
   uint64_t staged_begin = 0, staged_count = 0;
   // explicit schedule (psg_load_schedule)
@@ -619,6 +620,69 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
                       hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_prog + prog->n_words + prog->n_slots, prog->slot_flags, sizeof(int32_t) * prog->n_slots,
                       hipMemcpyHostToDevice));
+  // native lowering of the same Spec (round_amd/formula.py compile_native), if given
+  const bool native = prog->module_path != nullptr;
+  if (native && c->module_path != prog->module_path) {
+    if (c->module) (void)hipModuleUnload(c->module);
+    c->module = nullptr;
+    c->native_fn = nullptr;
+    c->fused_fn = c->fused_x_fn = nullptr;
+    c->module_path.clear();
+    HIPCHK(c, hipModuleLoad(&c->module, prog->module_path));
+    const std::string name = "psg_spec_native_w" + std::to_string(c->W);
+    HIPCHK(c, hipModuleGetFunction(&c->native_fn, c->module, name.c_str()));
+    // fused modules (compile_native(fused=True)) also hold the round kernel with the Spec as its hook
+    const std::string fw = "psg_fused_w" + std::to_string(c->W), fx = "psg_fused_x_w" + std::to_string(c->W);
+    if (hipModuleGetFunction(&c->fused_fn, c->module, fw.c_str()) != hipSuccess) c->fused_fn = nullptr;
+    if (hipModuleGetFunction(&c->fused_x_fn, c->module, fx.c_str()) != hipSuccess) c->fused_x_fn = nullptr;
+    (void)hipGetLastError();
+    c->module_path = prog->module_path;
+  }
+  if (native && (c->ho_loaded ? c->fused_x_fn : c->fused_fn)) {
+    // one launch: rounds + Spec from registers (no trace, no chunks)
+    hipFunction_t fn = c->ho_loaded ? c->fused_x_fn : c->fused_fn;
+    if (!(c->staged && c->staged_begin == inst_begin && c->staged_count == count)) {
+      int rc = psg_load_inputs(c, inst_begin, count, nullptr);
+      if (rc) return rc;
+    }
+    KArgs a = make_args(c);
+    a.inst_begin = inst_begin;
+    a.count = count;
+    a.init = c->d_init;
+    a.out_decision = c->d_dec;
+    a.out_dround = c->d_dround;
+    a.out_inst = c->d_inst;
+    const int threads = c->W == 1 ? 256 : 64 * c->W;
+    int per_cu = 0, cus = 0;
+    HIPCHK(c, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0));
+    HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->cfg.device));
+    const int G = groups_per_block(c->W);
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((count + G - 1) / G,
+                                                                           (uint64_t)cus * std::max(per_cu, 1)));
+    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, sizeof(unsigned long long) * NCOUNTERS_ALLOC, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    void* params[] = {&a};
+    HIPCHK(c, hipModuleLaunchKernel(fn, grid, 1, 1, (unsigned)threads, 1, 1, 0, c->stream, params, nullptr));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    unsigned long long host[NCOUNTERS_ALLOC];
+    HIPCHK(c, hipMemcpyAsync(host, c->d_counters, sizeof(host), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (out) {
+      out->instances = (int64_t)count;
+      out->process_rounds = (int64_t)count * c->cfg.n * c->cfg.rounds;
+      for (int i = 0; i < PSG_MAX_CHECKS; ++i) out->fail_count[i] = (int64_t)host[C_FAIL + i];
+      out->decided_processes = (int64_t)host[C_DECIDED];
+      out->digest = (int64_t)host[C_DIGEST];
+      for (int i = 0; i < R + 2; ++i) out->term_hist[i] = (int64_t)host[C_HIST + i];
+      out->kernel_ns = (int64_t)((double)ms * 1e6);
+    }
+    c->last_count = count;
+    if (per_inst)
+      HIPCHK(c, hipMemcpy(per_inst, c->d_inst, sizeof(psg_instance_summary) * count, hipMemcpyDeviceToHost));
+    return PSG_OK;
+  }
   // trace chunk: <= PSG_SPEC_TRACE_MB (default 2048) MiB of [R+1][fields][n] int32 rows
   uint64_t budget = 2048ull << 20;
   if (const char* e = std::getenv("PSG_SPEC_TRACE_MB")) {
@@ -638,18 +702,6 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
   if (!c->d_vm_err) HIPCHK(c, hipMalloc(&c->d_vm_err, sizeof(int32_t)));
   HIPCHK(c, hipMemsetAsync(c->d_vm_err, 0, sizeof(int32_t), c->stream));
   const bool staged = c->staged && c->staged_begin == inst_begin && c->staged_count == count;
-  // native lowering of the same Spec (round_amd/formula.py compile_native), if given
-  const bool native = prog->module_path != nullptr;
-  if (native && c->module_path != prog->module_path) {
-    if (c->module) (void)hipModuleUnload(c->module);
-    c->module = nullptr;
-    c->native_fn = nullptr;
-    c->module_path.clear();
-    HIPCHK(c, hipModuleLoad(&c->module, prog->module_path));
-    const std::string name = "psg_spec_native_w" + std::to_string(c->W);
-    HIPCHK(c, hipModuleGetFunction(&c->native_fn, c->module, name.c_str()));
-    c->module_path = prog->module_path;
-  }
   const uint32_t fields = prog_fields(prog);
   psg_summary acc;
   std::memset(&acc, 0, sizeof(acc));

@@ -39,8 +39,10 @@ PSG_DEV void benor_check(Grp<W>& g, Checks& ck, int c, bool has_old, int n, cons
   ck.record(fb, meq(D, full), c, g.lane);
 }
 
-template <int W, bool XHO>
-__global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
+// Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
+// fused Spec module (round_amd/formula.py compile_native(fused=True)).
+template <int W, bool XHO, class SH = NoHook>
+PSG_DEV void benor_body(const KArgs& a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[2 * W];
   __shared__ int64_t red[2 * W];
@@ -67,13 +69,14 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
     Checks ck;
     ck.reset();
-    benor_check<W>(g, ck, 0, false, n, full, x, cd, vote, decided, decision, false, false, true);
+    typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
+    if constexpr (!SH::kFused) benor_check<W>(g, ck, 0, false, n, full, x, cd, vote, decided, decision, false, false, true);
     // vote: Option[Boolean] (PSG_NONE32 when empty)
     auto trace = [&](int c, int32_t hs) {
-      trace_put<W>(g, a, i, c, x ? 1 : 0, decided ? 1 : 0, decision ? 1 : 0, 0, 0, 0, vote < 0 ? PSG_NONE32 : vote,
+      emit_state<W, SH>(sh, g, a, i, c, x ? 1 : 0, decided ? 1 : 0, decision ? 1 : 0, 0, 0, 0, vote < 0 ? PSG_NONE32 : vote,
                    cd ? 1 : 0, hs);
     };
-    if (a.trace) trace(0, n);
+    if (tracing<SH>(a)) trace(0, n);
     for (int k = 0; k < a.R; ++k) {
       const bool old_decided = decided, old_decision = decision;
       const Mask<W> act = g.ballot(!halted);
@@ -136,15 +139,21 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
         }
         if (halt_round == k) halted = true;
       }
-      benor_check<W>(g, ck, k + 1, true, n, full, x, cd, vote, decided, decision, old_decided, old_decision, pred);
-      if (a.trace) trace(k + 1, hs);
+      if constexpr (!SH::kFused) benor_check<W>(g, ck, k + 1, true, n, full, x, cd, vote, decided, decision, old_decided, old_decision, pred);
+      if (tracing<SH>(a)) trace(k + 1, hs);
     }
-    finish_instance<W>(g, a, i, ck, 5, dec_val, dec_round, halt_round, x ? 1 : 0, &bc);
+    finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 5, dec_val, dec_round, halt_round, x ? 1 : 0, &bc);
   }
   __syncthreads();
-  counters_flush(&bc, a.counters, 5, a.R);
+  counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 5, a.R);
 }
 
+template <int W, bool XHO, class SH = NoHook>
+__global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
+  benor_body<W, XHO, SH>(a);
+}
+
+#ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
   if (a.ho_in) hipLaunchKernelGGL((benor_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
@@ -171,5 +180,7 @@ const void* benor_kernel_ptr(int W) {
   }
   return nullptr;
 }
+
+#endif  // PSG_FUSED_MODULE
 
 }  // namespace psg

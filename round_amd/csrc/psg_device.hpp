@@ -844,6 +844,36 @@ PSG_DEV void trace_put(const Grp<W>& g, const KArgs& a, uint64_t i, int c, int32
   if (m & (1u << PSG_FIELD_HOSIZE)) t[PSG_FIELD_HOSIZE * n] = hosize;
 }
 
+// Spec hooks of the round kernels. NoHook: the built-in checks (+ the trace of
+// psg_run_batch_spec). A fused Spec module (round_amd/formula.py
+// compile_native(fused=True), psg_spec_native.hpp spec::SpecHook) instead
+// evaluates a compiled Spec at every check point from the kernel's registers.
+struct NoHook {
+  static constexpr bool kFused = false;
+  static constexpr int kSlots = 0;
+  template <int W>
+  struct State {
+    Checks ck;
+    PSG_DEV State(Grp<W>&, int, int) {}
+    PSG_DEV void put(int, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t) {}
+  };
+};
+
+// Is the process state of every check point needed (trace or fused Spec)?
+template <class SH>
+PSG_DEV bool tracing(const KArgs& a) {
+  return SH::kFused || a.trace != nullptr;
+}
+
+// One check point's process state: to the fused Spec, else to the trace.
+template <int W, class SH, class St>
+PSG_DEV void emit_state(St& sh, const Grp<W>& g, const KArgs& a, uint64_t i, int c, int32_t x, int32_t decided,
+                        int32_t decision, int32_t ts, int32_t ready, int32_t commit, int32_t vote, int32_t cand,
+                        int32_t hosize) {
+  if constexpr (SH::kFused) sh.put(c, x, decided, decision, ts, ready, commit, vote, cand, hosize);
+  else trace_put<W>(g, a, i, c, x, decided, decision, ts, ready, commit, vote, cand, hosize);
+}
+
 // Group geometry: W == 1 -> 4 independent instances per 256-thread block;
 // W > 1 -> one instance per block of 64*W threads.
 template <int W>

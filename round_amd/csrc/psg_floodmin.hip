@@ -17,8 +17,10 @@ struct FmLds {
   int32_t ds[W > 1 ? 64 * W : 1];
 };
 
-template <int W, bool XHO>
-__global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a) {
+// Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
+// fused Spec module (round_amd/formula.py compile_native(fused=True)).
+template <int W, bool XHO, class SH = NoHook>
+PSG_DEV void floodmin_body(const KArgs& a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[2 * W];
   __shared__ int64_t red[2 * W];
@@ -49,6 +51,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
     Checks ck;
     ck.reset();
+    typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
     auto check = [&](int c) {
       if constexpr (W > 1) {
         L.ds[g.pid] = decision;
@@ -56,11 +59,11 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
       }
       kagree_check<W>(g, ck, c, 1, full, decided, decision, X0, crashed, L.ds);
     };
-    check(0);
+    if constexpr (!SH::kFused) check(0);
     auto trace = [&](int c, int32_t hs) {
-      trace_put<W>(g, a, i, c, x, decided ? 1 : 0, decision, 0, 0, 0, 0, 0, hs);
+      emit_state<W, SH>(sh, g, a, i, c, x, decided ? 1 : 0, decision, 0, 0, 0, 0, 0, hs);
     };
-    if (a.trace) trace(0, n);
+    if (tracing<SH>(a)) trace(0, n);
     for (int k = 0; k < a.R; ++k) {
       const Mask<W> act = g.ballot(!halted);
       int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
@@ -73,7 +76,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
           CN = g.ballot(sc.crash_round == k);
         }
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
-        if (a.trace && !halted) hs = mpopc(M);
+        if (tracing<SH>(a) && !halted) hs = mpopc(M);
         // x = min(x, min{x_q : q in M}) by ascending distinct sender values
         bool unres = !halted;
         int32_t nx = x;
@@ -104,15 +107,21 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a
           }
         }
       }
-      check(k + 1);
-      if (a.trace) trace(k + 1, hs);
+      if constexpr (!SH::kFused) check(k + 1);
+      if (tracing<SH>(a)) trace(k + 1, hs);
     }
-    finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, x, &bc);
+    finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 2, dec_val, dec_round, halt_round, x, &bc);
   }
   __syncthreads();
-  counters_flush(&bc, a.counters, 2, a.R);
+  counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 2, a.R);
 }
 
+template <int W, bool XHO, class SH = NoHook>
+__global__ void __launch_bounds__(Geometry<W>::kThreads) floodmin_kernel(KArgs a) {
+  floodmin_body<W, XHO, SH>(a);
+}
+
+#ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
   if (a.ho_in) hipLaunchKernelGGL((floodmin_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
@@ -139,5 +148,7 @@ const void* floodmin_kernel_ptr(int W) {
   }
   return nullptr;
 }
+
+#endif  // PSG_FUSED_MODULE
 
 }  // namespace psg

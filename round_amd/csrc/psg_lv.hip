@@ -114,8 +114,10 @@ PSG_DEV Mask<W> ho_of(Grp<W>& g, LvLds<W>& L, const Mask<W>& ho, int c) {
   return m;
 }
 
-template <int W, bool XHO>
-__global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
+// Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
+// fused Spec module (round_amd/formula.py compile_native(fused=True)).
+template <int W, bool XHO, class SH = NoHook>
+PSG_DEV void lv_body(const KArgs& a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[2 * W];
   __shared__ int64_t red[2 * W];
@@ -149,12 +151,13 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
     Checks ck;
     ck.reset();
-    lv_check<W>(g, L, X0, ck, 0, false, n, full, x, ts, vote, decision, fl, 0u, -1);
+    typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
+    if constexpr (!SH::kFused) lv_check<W>(g, L, X0, ck, 0, false, n, full, x, ts, vote, decision, fl, 0u, -1);
     auto trace = [&](int c, int32_t hs) {
-      trace_put<W>(g, a, i, c, x, (fl & F_DECIDED) ? 1 : 0, decision, ts, (fl & F_READY) ? 1 : 0,
+      emit_state<W, SH>(sh, g, a, i, c, x, (fl & F_DECIDED) ? 1 : 0, decision, ts, (fl & F_READY) ? 1 : 0,
                    (fl & F_COMMIT) ? 1 : 0, vote, 0, hs);
     };
-    if (a.trace) trace(0, n);
+    if (tracing<SH>(a)) trace(0, n);
 
     for (int k = 0; k < a.R; ++k) {
       const uint32_t old_fl = fl;
@@ -225,15 +228,21 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
           }
         }
       }
-      lv_check<W>(g, L, X0, ck, k + 1, true, n, full, x, ts, vote, decision, fl, old_fl, old_decision);
-      if (a.trace) trace(k + 1, (old_fl & F_HALTED) ? n : hs);
+      if constexpr (!SH::kFused) lv_check<W>(g, L, X0, ck, k + 1, true, n, full, x, ts, vote, decision, fl, old_fl, old_decision);
+      if (tracing<SH>(a)) trace(k + 1, (old_fl & F_HALTED) ? n : hs);
     }
-    finish_instance<W>(g, a, i, ck, 7, dec_val, dec_round, halt_round, x, &bc);
+    finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 7, dec_val, dec_round, halt_round, x, &bc);
   }
   __syncthreads();
-  counters_flush(&bc, a.counters, 7, a.R);
+  counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 7, a.R);
 }
 
+template <int W, bool XHO, class SH = NoHook>
+__global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
+  lv_body<W, XHO, SH>(a);
+}
+
+#ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
   if (a.ho_in) hipLaunchKernelGGL((lv_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
@@ -260,5 +269,7 @@ const void* lv_kernel_ptr(int W) {
   }
   return nullptr;
 }
+
+#endif  // PSG_FUSED_MODULE
 
 }  // namespace psg

@@ -68,8 +68,10 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
   ck.record(fb, term, c, g.lane);
 }
 
-template <int W, bool V2, bool XHO>
-__global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
+// Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
+// fused Spec module (round_amd/formula.py compile_native(fused=True)).
+template <int W, bool V2, bool XHO, class SH = NoHook>
+PSG_DEV void otr_body(const KArgs& a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[2 * W];
   __shared__ int64_t red[2 * W];
@@ -103,12 +105,13 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
     Checks ck;
     ck.reset();
-    otr_check<W, V2>(g, L, X0, ck, 0, false, n, full, x, dec01, decision, 0u, -1, valid01);
+    typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
+    if constexpr (!SH::kFused) otr_check<W, V2>(g, L, X0, ck, 0, false, n, full, x, dec01, decision, 0u, -1, valid01);
     // OTR2's decision is an Option (PSG_NONE32 when empty)
     auto trace = [&](int c, int32_t hs) {
-      trace_put<W>(g, a, i, c, x, (int32_t)dec01, V2 && !dec01 ? PSG_NONE32 : decision, 0, 0, 0, 0, 0, hs);
+      emit_state<W, SH>(sh, g, a, i, c, x, (int32_t)dec01, V2 && !dec01 ? PSG_NONE32 : decision, 0, 0, 0, 0, 0, hs);
     };
-    if (a.trace) trace(0, n);
+    if (tracing<SH>(a)) trace(0, n);
     pt.mark(0);
 
     for (int k = 0; k < a.R; ++k) {
@@ -127,7 +130,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
         // mailbox: broadcast(x) from every alive sender in HO(p)
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const int32_t msize = mpopc(M);
-        if (a.trace) hs = halted01 ? n : msize;
+        if (tracing<SH>(a)) hs = halted01 ? n : msize;
         const uint32_t upd = (1u - halted01) & gt01(msize, thr);
         if (g.any(upd != 0u)) {
           if constexpr (W > 1) {
@@ -163,18 +166,25 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) otr_kernel(KArgs a) {
         halt_round = h ? k : halt_round;
         halted01 |= h;
       }
-      otr_check<W, V2>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, old01, old_decision, valid01);
-      if (a.trace) trace(k + 1, hs);
+      if constexpr (!SH::kFused) otr_check<W, V2>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, old01, old_decision, valid01);
+      if (tracing<SH>(a)) trace(k + 1, hs);
       pt.mark(many(act) ? 1 : 2);
     }
-    finish_instance<W>(g, a, i, ck, 8, dec_val, dec_round, halt_round, x, &bc);
+    finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 8, dec_val, dec_round, halt_round, x, &bc);
     pt.mark(3);
   }
   pt.flush(a.counters, threadIdx.x & 63);
   __syncthreads();
-  counters_flush(&bc, a.counters, 8, a.R);
+  counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 8, a.R);
 }
 
+template <int W, bool V2, bool XHO, class SH = NoHook>
+__global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? 6 : 1)))
+otr_kernel(KArgs a) {
+  otr_body<W, V2, XHO, SH>(a);
+}
+
+#ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W, bool V2>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
   if (a.ho_in) hipLaunchKernelGGL((otr_kernel<W, V2, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
@@ -208,5 +218,7 @@ hipError_t launch_otr(const KArgs& a, int W, int grid, hipStream_t s) { return l
 hipError_t launch_otr2(const KArgs& a, int W, int grid, hipStream_t s) { return launch_v<true>(a, W, grid, s); }
 const void* otr_kernel_ptr(int W) { return ptr_v<false>(W); }
 const void* otr2_kernel_ptr(int W) { return ptr_v<true>(W); }
+
+#endif  // PSG_FUSED_MODULE
 
 }  // namespace psg

@@ -51,8 +51,10 @@ PSG_DEV Mask<W> slv_ho_of(Grp<W>& g, SlvLds<W>& L, const Mask<W>& ho, int c) {
   return m;
 }
 
-template <int W, bool XHO>
-__global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
+// Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
+// fused Spec module (round_amd/formula.py compile_native(fused=True)).
+template <int W, bool XHO, class SH = NoHook>
+PSG_DEV void slv_body(const KArgs& a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[2 * W];
   __shared__ int64_t red[2 * W];
@@ -86,6 +88,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
     Checks ck;
     ck.reset();
+    typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
     auto check = [&](int c) {
       if constexpr (W > 1) {
         L.ds[g.pid] = decision;
@@ -93,11 +96,11 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
       }
       kagree_check<W>(g, ck, c, 1, full, (fl & S_DECIDED) != 0u, decision, X0, false, L.ds);
     };
-    check(0);
+    if constexpr (!SH::kFused) check(0);
     auto trace = [&](int c, int32_t hs) {
-      trace_put<W>(g, a, i, c, x, (fl & S_DECIDED) ? 1 : 0, decision, ts, 0, (fl & S_COMMIT) ? 1 : 0, vote, 0, hs);
+      emit_state<W, SH>(sh, g, a, i, c, x, (fl & S_DECIDED) ? 1 : 0, decision, ts, 0, (fl & S_COMMIT) ? 1 : 0, vote, 0, hs);
     };
-    if (a.trace) trace(0, n);
+    if (tracing<SH>(a)) trace(0, n);
 
     for (int k = 0; k < a.R; ++k) {
       const Mask<W> act = g.ballot((fl & S_HALTED) == 0u);
@@ -171,15 +174,21 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
           }
         }
       }
-      check(k + 1);
-      if (a.trace) trace(k + 1, (fl_start & S_HALTED) ? n : hs);
+      if constexpr (!SH::kFused) check(k + 1);
+      if (tracing<SH>(a)) trace(k + 1, (fl_start & S_HALTED) ? n : hs);
     }
-    finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, x, &bc);
+    finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 2, dec_val, dec_round, halt_round, x, &bc);
   }
   __syncthreads();
-  counters_flush(&bc, a.counters, 2, a.R);
+  counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 2, a.R);
 }
 
+template <int W, bool XHO, class SH = NoHook>
+__global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
+  slv_body<W, XHO, SH>(a);
+}
+
+#ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
   if (a.ho_in) hipLaunchKernelGGL((slv_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
@@ -225,5 +234,7 @@ hipError_t launch_champ_selftest(const uint64_t* sets, int count, int tiebreak, 
   hipLaunchKernelGGL(champ_selftest_kernel, dim3((count + 255) / 256), dim3(256), 0, s, sets, count, tiebreak, out);
   return hipGetLastError();
 }
+
+#endif  // PSG_FUSED_MODULE
 
 }  // namespace psg

@@ -398,6 +398,71 @@ __device__ void native_kernel_body(const VmArgs& A) {
   counters_flush(&bc, A.counters, S::kSlots, A.R);
 }
 
+// ---------------------------------------------------------------- fused round kernel hook
+// compile_native(fused=True): the algorithm's round kernel is instantiated with
+// SpecHook<S> and evaluates S at every check point from its own registers — the
+// same per-process values psg_run_batch_spec would trace (emit_state), so the
+// results are those of the trace + native_kernel_body path without the trace's
+// HBM round trip and second launch.
+template <class S>
+struct SpecHook {
+  static constexpr bool kFused = true;
+  static constexpr int kSlots = S::kSlots;
+  template <int W>
+  struct State {
+    Ctx<W> x;
+    Checks ck;
+    int grp;
+    PSG_DEV static int32_t* stage_lds() {
+      __shared__ int32_t b[W > 1 ? 3 * PSG_NFIELDS * 64 * W : 1];
+      return b;
+    }
+    PSG_DEV static int32_t* scratch_lds(int grp) {
+      __shared__ int32_t b[Geometry<W>::kGroups][64 * W];
+      return b[grp];
+    }
+    PSG_DEV static int32_t* iset_lds(int k, int grp) {
+      __shared__ int32_t b[S::kInitSet0 >= 0 ? (S::kInitSet1 >= 0 ? 2 : 1) : 1][Geometry<W>::kGroups]
+                          [S::kInitSet0 >= 0 ? X0Set<W>::kSlots : 1];
+      return b[k][grp];
+    }
+    PSG_DEV State(Grp<W>& g, int grp_, int n) : x{g, n, 0, {0}, {0}, {0}, stage_lds()}, grp(grp_) { ck.reset(); }
+
+    PSG_DEV void put(int c, int32_t f0, int32_t f1, int32_t f2, int32_t f3, int32_t f4, int32_t f5, int32_t f6,
+                     int32_t f7, int32_t f8) {
+      Grp<W>& g = x.g;
+      const int32_t v[PSG_NFIELDS] = {f0, f1, f2, f3, f4, f5, f6, f7, f8};
+      x.r = c;
+      x.maj_k0 = x.maj_k1 = -1;
+#pragma unroll
+      for (int f = 0; f < PSG_NFIELDS; ++f) {
+        if (!((S::kFields >> f) & 1u)) continue;
+        const int32_t val = g.valid ? v[f] : 0;  // the trace holds valid processes only
+        if (c == 0) {
+          x.i[f] = val;
+          if constexpr (W > 1) x.sc[(PSG_TAG_INIT * PSG_NFIELDS + f) * 64 * W + g.pid] = val;
+        }
+        x.o[f] = c == 0 ? val : x.c[f];
+        x.c[f] = val;
+        if constexpr (W > 1) {
+          x.sc[(PSG_TAG_OLD * PSG_NFIELDS + f) * 64 * W + g.pid] = x.o[f];
+          x.sc[(PSG_TAG_CUR * PSG_NFIELDS + f) * 64 * W + g.pid] = val;
+        }
+      }
+      if (c == 0) {
+        if constexpr (S::kInitSet0 >= 0) x.iset[0].build(g, iset_lds(0, grp), x.i[S::kInitSet0]);
+        if constexpr (S::kInitSet1 >= 0) x.iset[1].build(g, iset_lds(1, grp), x.i[S::kInitSet1]);
+      }
+      if constexpr (W > 1) __syncthreads();
+      uint32_t fb = S::template fail<W>(x, scratch_lds(grp));
+      if (c == 0) fb &= ~S::kRelational;
+      const bool term = S::kHasTerm && S::template term<W>(x, scratch_lds(grp));
+      ck.record(fb, term, c, g.lane);
+      if constexpr (W > 1) __syncthreads();
+    }
+  };
+};
+
 }  // namespace spec
 }  // namespace psg
 

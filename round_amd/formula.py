@@ -1007,17 +1007,57 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
     return "\n".join(src), prog
 
 
-def compile_native(spec: Spec, alg: Optional[int] = None, cache_dir: str = None, hipcc: str = None) -> Program:
+# algorithm -> (round-kernel source, body template, leading template arguments) for fused modules
+FUSED_KERNELS = {
+    abi.PSG_ALG_OTR: ("psg_otr.hip", "otr_body", "{W}, false"),
+    abi.PSG_ALG_OTR2: ("psg_otr.hip", "otr_body", "{W}, true"),
+    abi.PSG_ALG_LAST_VOTING: ("psg_lv.hip", "lv_body", "{W}"),
+    abi.PSG_ALG_FLOODMIN: ("psg_floodmin.hip", "floodmin_body", "{W}"),
+    abi.PSG_ALG_KSET: ("psg_kset.hip", "kset_body", "{W}"),
+    abi.PSG_ALG_BENOR: ("psg_benor.hip", "benor_body", "{W}"),
+    abi.PSG_ALG_SLV: ("psg_slv.hip", "slv_body", "{W}"),
+    abi.PSG_ALG_KSET_ES: ("psg_kset_es.hip", "kset_es_body", "{W}"),
+}
+
+
+def _fused_source(alg: int, waves: Sequence[int]) -> str:
+    """The algorithm's round kernel instantiated with the generated Spec as its hook:
+    extern "C" psg_fused_w<W> (seeded HO sets) / psg_fused_x_w<W> (explicit)."""
+    src, body, targs = FUSED_KERNELS[alg]
+    out = [f'#include "{src}"  // its kernel bodies; host launchers are compiled out (PSG_FUSED_MODULE)']
+    for W in waves:
+        threads = 256 if W == 1 else 64 * W
+        for suffix, xho in (("", "false"), ("x_", "true")):
+            out.append(f'extern "C" __global__ void __launch_bounds__({threads}) psg_fused_{suffix}w{W}(psg::KArgs a) {{')
+            out.append(f"  psg::{body}<{targs.format(W=W)}, {xho}, psg::spec::SpecHook<psg::GenSpec>>(a);")
+            out.append("}")
+    return "\n".join(out) + "\n"
+
+
+def compile_native(spec: Spec, alg: Optional[int] = None, cache_dir: str = None, hipcc: str = None,
+                   fused: bool = False, n: Optional[int] = None) -> Program:
     """Lower `spec` to native gfx950 code (hipcc --genco, cached by source hash) and
     return a Program whose module_path psg_run_batch_spec launches instead of the
-    bytecode interpreter."""
+    bytecode interpreter.
+
+    fused=True also instantiates the algorithm's round kernel with the Spec as its
+    check hook (spec::SpecHook): psg_run_batch_spec then runs ONE launch that
+    executes the rounds and evaluates the Spec from registers, with no state trace.
+    `n` (optional) limits the instantiations to that group size's wave count."""
     import hashlib
     import os
     import subprocess
     src, prog = codegen_hip(spec, alg)
+    hdr_names = ["psg_spec_native.hpp", "psg_device.hpp"]
+    if fused:
+        if alg not in FUSED_KERNELS:
+            raise FormulaError("fused lowering needs one of the integer-state algorithms")
+        waves = [(n + 63) // 64] if n is not None else [1, 2, 3, 4]
+        src = "#define PSG_FUSED_MODULE 1\n" + src + _fused_source(alg, waves)
+        hdr_names.append(FUSED_KERNELS[alg][0])
     cache_dir = cache_dir or CACHE_DIR
     os.makedirs(cache_dir, exist_ok=True)
-    hdrs = "".join(open(os.path.join(_CSRC, h)).read() for h in ("psg_spec_native.hpp", "psg_device.hpp"))
+    hdrs = "".join(open(os.path.join(_CSRC, h)).read() for h in hdr_names)
     key = hashlib.sha256((src + hdrs + open(os.path.join(_INCLUDE, "psg.h")).read()).encode()).hexdigest()[:24]
     out = os.path.join(cache_dir, f"spec_{key}.co")
     if not os.path.exists(out):

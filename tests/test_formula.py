@@ -90,3 +90,15 @@ def test_native_lowering_builds(name):
     prog = F.compile_native(mk(), alg)
     import os
     assert os.path.getsize(prog.module_path) > 1000
+
+
+@pytest.mark.parametrize("alg", sorted(F.FUSED_KERNELS), ids=lambda a: abi.CHECK_NAMES and str(a))
+def test_fused_lowering_builds(alg):
+    """compile_native(fused=True): each integer-state round kernel instantiated with a
+    generated Spec hook compiles for gfx950 (both HO-set sources, one wave count)."""
+    spec = F.REFERENCE_SPECS[alg]() if alg in F.REFERENCE_SPECS else spec_cases.uniform_agreement()
+    prog = F.compile_native(spec, alg, fused=True, n=64)
+    import os
+    assert os.path.getsize(prog.module_path) > 1000
+    src = open(prog.module_path[:-3] + ".hip").read()
+    assert "psg_fused_w1" in src and "psg_fused_x_w1" in src

@@ -149,9 +149,11 @@ def test_schedule_range_errors():
         g.run(95, I)
 
 
-def test_spec_program_under_explicit_schedule(oracle_mod):
+@pytest.mark.parametrize("mode", ["vm", "fused"])
+def test_spec_program_under_explicit_schedule(oracle_mod, mode):
     """psg_run_batch_spec reads the loaded schedule too: the reference OTR Spec
-    compiled from the DSL equals the built-in checks on the same explicit sets."""
+    compiled from the DSL (interpreted, or fused into the explicit-schedule round
+    kernel) equals the built-in checks on the same explicit sets."""
     from round_amd import formula
     n, R, I = 64, 10, 200
     rng = np.random.default_rng(3)
@@ -161,7 +163,9 @@ def test_spec_program_under_explicit_schedule(oracle_mod):
         g._ctx.load_inputs(0, I, init)
         g.load_schedule(0, I, ho)
         _, pi = g._ctx.run_batch_np(0, I)
-        sr = g.run_spec(0, I, formula.otr_spec(), per_instance=True)
+        spec = formula.otr_spec() if mode == "vm" else formula.compile_native(formula.otr_spec(), abi.PSG_ALG_OTR,
+                                                                               fused=True, n=n)
+        sr = g.run_spec(0, I, spec, per_instance=True)
     for a, b in zip(pi, sr.per_instance):
         assert list(a["first_fail"][:8]) == list(b.first_fail)[:8]
         assert int(a["term_round"]) == b.term_round

@@ -34,14 +34,16 @@ def _rows(pi, k):
     return [(tuple(s.first_fail)[:k], s.term_round) for s in pi]
 
 
-def _prog(spec, alg_id, mode):
+def _prog(spec, alg_id, mode, n=None):
+    if mode == "fused":  # the round kernel instantiated with the Spec as its hook: no trace
+        return F.compile_native(spec, alg_id, fused=True, n=n)
     return F.compile_native(spec, alg_id) if mode == "native" else F.compile_spec(spec, alg_id)
 
 
-@pytest.mark.parametrize("mode", ["vm", "native"])
+@pytest.mark.parametrize("mode", ["vm", "native", "fused"])
 @pytest.mark.parametrize("cid,alg,n,count,kw", REF, ids=[c[0] for c in REF])
 def test_reference_spec_program_matches_builtin_checks(cid, alg, n, count, kw, mode):
-    prog = _prog(F.REFERENCE_SPECS[alg.alg_id](), alg.alg_id, mode)
+    prog = _prog(F.REFERENCE_SPECS[alg.alg_id](), alg.alg_id, mode, n)
     k = len(prog.slot_names)
     with psync.GpuRound(alg, n, batch_capacity=count, **kw) as gr:
         built = gr.run(0, count, per_instance=True)
@@ -52,10 +54,10 @@ def test_reference_spec_program_matches_builtin_checks(cid, alg, n, count, kw, m
     assert spec.summary.digest == built.summary.digest
 
 
-@pytest.mark.parametrize("mode", ["vm", "native"])
+@pytest.mark.parametrize("mode", ["vm", "native", "fused"])
 @pytest.mark.parametrize("cid,alg,n,kw,mk", spec_cases.CUSTOM, ids=[c[0] for c in spec_cases.CUSTOM])
 def test_custom_spec_matches_cpu_interpreter(cid, alg, n, kw, mk, oracle_mod, mode):
-    prog = _prog(mk(), alg.alg_id, mode)
+    prog = _prog(mk(), alg.alg_id, mode, n)
     count = 300 if n <= 16 else 60
     with psync.GpuRound(alg, n, batch_capacity=count, seed=19, **kw) as gr:
         res = gr.run_spec(100, count, prog, per_instance=True)
