@@ -12,6 +12,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/psg.h"
 #include "psg_device.hpp"
@@ -132,6 +133,32 @@ static int hip_fail(psg_ctx* c, hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
   } while (0)
 
+// Profiling builds (-DPSG_PHASE_TIMERS=1): per-phase cycles, shader clock, wave lifetimes.
+static void print_timers(const unsigned long long* host) {
+  if (!PSG_PHASE_TIMERS) return;
+  const unsigned long long* t = host + C_TIMER;
+  const unsigned long long waves = t[7], t0 = ~t[5], span = t[6] - ~t[5];
+  std::fprintf(stderr, "psg phase cycles: setup %llu active %llu check_only %llu finish %llu\n", t[0], t[1], t[2], t[3]);
+  std::fprintf(stderr, "psg wave lifetime: waves %llu, sum %llu rt ticks (100 MHz), span %llu ticks, mean/span %.3f, "
+               "shader clock %.3f GHz\n", waves, t[4], span, waves ? (double)t[4] / waves / (double)span : 0.0,
+               t[4] ? 0.1 * (t[0] + t[1] + t[2] + t[3]) / (double)t[4] : 0.0);
+  // deciles of wave start and end times, as fractions of the span
+  const size_t m = std::min<unsigned long long>(waves, NSTAMP_WAVES);
+  std::vector<double> st(m), en(m);
+  for (size_t w = 0; w < m; ++w) {
+    st[w] = (double)(t[8 + 2 * w] - t0) / span;
+    en[w] = (double)(t[9 + 2 * w] - t0) / span;
+  }
+  std::sort(st.begin(), st.end());
+  std::sort(en.begin(), en.end());
+  if (!m) return;
+  std::fprintf(stderr, "psg wave start deciles:");
+  for (int d = 0; d <= 10; ++d) std::fprintf(stderr, " %.3f", st[std::min(m - 1, d * m / 10)]);
+  std::fprintf(stderr, "\npsg wave end deciles:  ");
+  for (int d = 0; d <= 10; ++d) std::fprintf(stderr, " %.3f", en[std::min(m - 1, d * m / 10)]);
+  std::fprintf(stderr, "\n");
+}
+
 static hipError_t launch_alg(const psg_ctx* c, const KArgs& a, int grid) {
   switch (c->cfg.alg) {
     case PSG_ALG_OTR: return launch_otr(a, c->W, grid, c->stream);
@@ -212,9 +239,7 @@ static int run_kernel(psg_ctx* c, KArgs& a, uint64_t count, psg_summary* out, bo
   unsigned long long host[NCOUNTERS_ALLOC];
   HIPCHK(c, hipMemcpyAsync(host, c->d_counters, sizeof(host), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (PSG_PHASE_TIMERS && std::getenv("PSG_PHASE_TIMERS"))  // profiling builds: cycles per phase
-    std::fprintf(stderr, "psg phase cycles: setup %llu active %llu check_only %llu finish %llu\n", host[C_TIMER],
-                 host[C_TIMER + 1], host[C_TIMER + 2], host[C_TIMER + 3]);
+  if (PSG_PHASE_TIMERS && std::getenv("PSG_PHASE_TIMERS")) print_timers(host);
   if (out) {
     std::memset(out, 0, sizeof(*out));
     out->instances = (int64_t)count;

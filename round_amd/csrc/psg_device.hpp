@@ -86,22 +86,29 @@ struct PopArgs {
   int benor;
 };
 
+#ifndef PSG_PHASE_TIMERS
+#define PSG_PHASE_TIMERS 0
+#endif
 // global counter layout (uint64 each)
 enum { C_FAIL = 0, C_DECIDED = PSG_MAX_CHECKS, C_DIGEST = PSG_MAX_CHECKS + 1, C_HIST = PSG_MAX_CHECKS + 2,
        NCOUNTERS = C_HIST + PSG_MAX_ROUNDS + 2,
        // profiling builds only (-DPSG_PHASE_TIMERS=1): per-phase shader cycles summed over waves
-       C_TIMER = NCOUNTERS, NTIMERS = 4, NCOUNTERS_ALLOC = NCOUNTERS + NTIMERS };
+       // (4 phase slots, then wave-lifetime s_memrealtime ticks summed, ~min start, max end, waves)
+       // (4 phase slots, then wave-lifetime s_memrealtime ticks summed, ~min start, max end, waves,
+       // then (start, end) per wave for the first 16384 waves)
+       // instance queues (InstanceQueue): NQUEUES counters, one per 128 B line
+       C_QUEUE = NCOUNTERS, NQUEUES = 8, QUEUE_STRIDE = 16,
+       C_TIMER = C_QUEUE + NQUEUES * QUEUE_STRIDE, NTIMERS = 4, NSTAMP_WAVES = 16384,
+       NTIMER_SLOTS = PSG_PHASE_TIMERS ? 8 + 2 * NSTAMP_WAVES : 0, NCOUNTERS_ALLOC = C_TIMER + NTIMER_SLOTS };
 
-#ifndef PSG_PHASE_TIMERS
-#define PSG_PHASE_TIMERS 0
-#endif
 // Phase timers of a profiling build: t.mark(j) charges the cycles since the last
 // mark to phase j (uniform, kept in SGPRs); flush adds them to the global slots.
 struct PhaseTimers {
 #if PSG_PHASE_TIMERS
-  uint64_t last, acc[NTIMERS];
+  uint64_t last, rt0, acc[NTIMERS];
   PSG_DEV void start() {
     for (int j = 0; j < NTIMERS; ++j) acc[j] = 0;
+    rt0 = __builtin_amdgcn_s_memrealtime();
     last = __builtin_amdgcn_s_memtime();
   }
   PSG_DEV void mark(int j) {
@@ -110,8 +117,19 @@ struct PhaseTimers {
     last = t;
   }
   PSG_DEV void flush(unsigned long long* g, int lane) {
-    if (lane == 0)
+    const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
       for (int j = 0; j < NTIMERS; ++j) atomicAdd(&g[C_TIMER + j], (unsigned long long)acc[j]);
+      atomicAdd(&g[C_TIMER + 4], (unsigned long long)(rt1 - rt0));
+      atomicMax(&g[C_TIMER + 5], (unsigned long long)~rt0);
+      atomicMax(&g[C_TIMER + 6], (unsigned long long)rt1);
+      atomicAdd(&g[C_TIMER + 7], 1ull);
+      const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+      if (wave < NSTAMP_WAVES) {
+        g[C_TIMER + 8 + 2 * wave] = rt0;
+        g[C_TIMER + 9 + 2 * wave] = rt1;
+      }
+    }
   }
 #else
   PSG_DEV void start() {}
@@ -554,6 +572,66 @@ PSG_DEV void lds_sync() {
     __builtin_amdgcn_wave_barrier();
   }
 }
+
+// ---------------------------------------------------------------- instance queue
+// Dynamic distribution of a batch's instances over the resident groups.
+// A static grid-stride split left the chip 30% idle on the headline launch: a
+// SIMD issues by wave age, so its six resident waves run at very different
+// speeds (timer build, profiles/s2_queue: the oldest wave of a SIMD finishes at
+// 0.45 of the kernel span, the youngest at 1.0, in six steps), and each SIMD
+// ran the second half of the launch with fewer and fewer waves to hide latency.
+// Here a group takes kChunk consecutive instances at a time from one of
+// NQUEUES counters (queue = blockIdx % NQUEUES, which spreads the atomics over
+// the XCDs the blocks are dispatched to round-robin; queue q owns the slice
+// [q*count/NQUEUES, (q+1)*count/NQUEUES)) and moves to the next queue when its
+// own is drained, so every group works until the whole batch is done. Which
+// group runs an instance does not change any result: per-instance outputs are
+// indexed by the instance's batch row, counters are integer sums.
+// The counters live in a.counters[C_QUEUE + q*QUEUE_STRIDE], zeroed before
+// every launch together with the result counters.
+template <int W>
+struct InstanceQueue {
+  static constexpr uint64_t kChunk = W == 1 ? 4 : 1;
+  static constexpr uint64_t kDone = ~0ull;
+  uint64_t cur = 0, lim = 0;  // uniform: [cur, lim) is this group's current chunk
+  int tries = 0;              // queues drained so far
+
+  // Next batch row of this group, kDone when the whole batch is taken.
+  // Called by every lane of the group in converged control flow.
+  PSG_DEV uint64_t take(const KArgs& a) {
+    if (cur < lim) return cur++;
+    const int home = (int)(blockIdx.x % NQUEUES);
+    for (; tries < NQUEUES; ++tries) {
+      const int q = (home + tries) % NQUEUES;
+      const uint64_t lo = a.count * q / NQUEUES, hi = a.count * (q + 1) / NQUEUES;
+      if (lo >= hi) continue;
+      const uint64_t v = grab(&a.counters[C_QUEUE + q * QUEUE_STRIDE]);
+      if (lo + v < hi) {
+        cur = lo + v;
+        lim = cur + kChunk < hi ? cur + kChunk : hi;
+        return cur++;
+      }
+    }
+    return kDone;
+  }
+
+ private:
+  // one atomic per group, its old value broadcast to every lane of the group
+  PSG_DEV static uint64_t grab(unsigned long long* c) {
+    if constexpr (W == 1) {
+      uint64_t v = 0;
+      if ((threadIdx.x & 63) == 0) v = atomicAdd(c, (unsigned long long)kChunk);
+      return rfl64(v);
+    } else {
+      __shared__ uint64_t slot;
+      if (threadIdx.x == 0) slot = atomicAdd(c, (unsigned long long)kChunk);
+      __syncthreads();
+      const uint64_t v = rfl64(slot);
+      __syncthreads();  // slot is rewritten by the next grab
+      return v;
+    }
+  }
+};
 
 // ---------------------------------------------------------------- schedule
 // XHO: explicit schedule (psg_load_schedule) — HO sets read from HBM instead of

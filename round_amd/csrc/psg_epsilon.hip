@@ -75,7 +75,6 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a)
   __syncthreads();
   Grp<W> g;
   grp_setup(g, a, xb, red);
-  constexpr int G = Geometry<W>::kGroups;
   // wave-uniform group index (SGPR): measured +3% on this kernel (fewer VGPRs, one more wave/SIMD);
   // the same change cost OTR / ShortLastVoting 1-3%, which keep the VGPR form
   const int grp = W == 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
@@ -87,7 +86,8 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a)
   double* sx = L.sx[grp];
   int32_t* spid = L.spid[grp];
 
-  for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
+  InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
+  for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);

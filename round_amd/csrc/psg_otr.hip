@@ -81,7 +81,6 @@ PSG_DEV void otr_body(const KArgs& a) {
   __syncthreads();
   Grp<W> g;
   grp_setup(g, a, xb, red);
-  constexpr int G = Geometry<W>::kGroups;
   const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
   const int n = a.n;
   const int thr = a.variant == 1 ? n / 2 : (2 * n) / 3;  // Otr.scala:64, 67 (variant 1: mutation)
@@ -90,7 +89,8 @@ PSG_DEV void otr_body(const KArgs& a) {
 
   PhaseTimers pt;  // profiling builds only
   pt.start();
-  for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
+  InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
+  for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);

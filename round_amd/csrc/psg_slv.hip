@@ -66,14 +66,14 @@ PSG_DEV void slv_body(const KArgs& a) {
   __syncthreads();
   Grp<W> g;
   grp_setup(g, a, xb, red);
-  constexpr int G = Geometry<W>::kGroups;
   const int grp = W == 1 ? (int)(threadIdx.x >> 6) : 0;
   const int n = a.n;
   const int need2 = a.variant == 1 ? 0 : n / 2;  // R2 quorum (ShortLastVoting.scala:85; variant 1: mutation)
   const Mask<W> full = mfull<W>(n);
   const uint32_t myh = scala_improve((uint32_t)g.pid);
 
-  for (uint64_t i = (uint64_t)blockIdx.x * G + grp; i < a.count; i += (uint64_t)gridDim.x * G) {
+  InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
+  for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
