@@ -182,7 +182,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": "psg::otr_kernel<1, false, false>",  # <W, OTR2, explicit schedule>
+                "kernel": "psg::otr_kernel<1, false, false, psg::NoHook>",  # <W, OTR2, explicit schedule, check hook>
                 "kernel_ms": head["kernel_s"] * 1e3,
                 "bytes_per_process_round": B_ALG_OTR,
             },

@@ -137,17 +137,24 @@ static int hip_fail(psg_ctx* c, hipError_t e, const char* what) {
 static void print_timers(const unsigned long long* host) {
   if (!PSG_PHASE_TIMERS) return;
   const unsigned long long* t = host + C_TIMER;
-  const unsigned long long waves = t[7], t0 = ~t[5], span = t[6] - ~t[5];
-  std::fprintf(stderr, "psg phase cycles: setup %llu active %llu check_only %llu finish %llu\n", t[0], t[1], t[2], t[3]);
+  const unsigned long long waves = t[T_WAVES], t0 = ~t[T_RT_MIN], span = t[T_RT_MAX] - ~t[T_RT_MIN];
+  unsigned long long cyc = 0;
+  std::fprintf(stderr, "psg phase cycles (kernel's own phase map):");
+  for (int j = 0; j < NTIMERS; ++j) {
+    std::fprintf(stderr, " t%d %llu", j, t[j]);
+    cyc += t[j];
+  }
+  std::fprintf(stderr, "\n");
   std::fprintf(stderr, "psg wave lifetime: waves %llu, sum %llu rt ticks (100 MHz), span %llu ticks, mean/span %.3f, "
-               "shader clock %.3f GHz\n", waves, t[4], span, waves ? (double)t[4] / waves / (double)span : 0.0,
-               t[4] ? 0.1 * (t[0] + t[1] + t[2] + t[3]) / (double)t[4] : 0.0);
+               "shader clock %.3f GHz\n", waves, t[T_RT_SUM], span,
+               waves ? (double)t[T_RT_SUM] / waves / (double)span : 0.0,
+               t[T_RT_SUM] ? 0.1 * cyc / (double)t[T_RT_SUM] : 0.0);
   // deciles of wave start and end times, as fractions of the span
   const size_t m = std::min<unsigned long long>(waves, NSTAMP_WAVES);
   std::vector<double> st(m), en(m);
   for (size_t w = 0; w < m; ++w) {
-    st[w] = (double)(t[8 + 2 * w] - t0) / span;
-    en[w] = (double)(t[9 + 2 * w] - t0) / span;
+    st[w] = (double)(t[T_STAMPS + 2 * w] - t0) / span;
+    en[w] = (double)(t[T_STAMPS + 1 + 2 * w] - t0) / span;
   }
   std::sort(st.begin(), st.end());
   std::sort(en.begin(), en.end());

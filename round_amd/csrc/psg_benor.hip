@@ -44,7 +44,7 @@ PSG_DEV void benor_check(Grp<W>& g, Checks& ck, int c, bool has_old, int n, cons
 template <int W, bool XHO, class SH = NoHook>
 PSG_DEV void benor_body(const KArgs& a) {
   __shared__ BlockCounters bc;
-  __shared__ uint64_t xb[2 * W];
+  __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int64_t red[2 * W];
   counters_init(&bc);
   __syncthreads();

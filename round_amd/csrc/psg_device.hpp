@@ -98,8 +98,10 @@ enum { C_FAIL = 0, C_DECIDED = PSG_MAX_CHECKS, C_DIGEST = PSG_MAX_CHECKS + 1, C_
        // then (start, end) per wave for the first 16384 waves)
        // instance queues (InstanceQueue): NQUEUES counters, one per 128 B line
        C_QUEUE = NCOUNTERS, NQUEUES = 8, QUEUE_STRIDE = 16,
-       C_TIMER = C_QUEUE + NQUEUES * QUEUE_STRIDE, NTIMERS = 4, NSTAMP_WAVES = 16384,
-       NTIMER_SLOTS = PSG_PHASE_TIMERS ? 8 + 2 * NSTAMP_WAVES : 0, NCOUNTERS_ALLOC = C_TIMER + NTIMER_SLOTS };
+       C_TIMER = C_QUEUE + NQUEUES * QUEUE_STRIDE, NTIMERS = 6, NSTAMP_WAVES = 16384,
+       T_RT_SUM = NTIMERS, T_RT_MIN = NTIMERS + 1, T_RT_MAX = NTIMERS + 2, T_WAVES = NTIMERS + 3,
+       T_STAMPS = NTIMERS + 4,
+       NTIMER_SLOTS = PSG_PHASE_TIMERS ? T_STAMPS + 2 * NSTAMP_WAVES : 0, NCOUNTERS_ALLOC = C_TIMER + NTIMER_SLOTS };
 
 // Phase timers of a profiling build: t.mark(j) charges the cycles since the last
 // mark to phase j (uniform, kept in SGPRs); flush adds them to the global slots.
@@ -120,14 +122,14 @@ struct PhaseTimers {
     const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
       for (int j = 0; j < NTIMERS; ++j) atomicAdd(&g[C_TIMER + j], (unsigned long long)acc[j]);
-      atomicAdd(&g[C_TIMER + 4], (unsigned long long)(rt1 - rt0));
-      atomicMax(&g[C_TIMER + 5], (unsigned long long)~rt0);
-      atomicMax(&g[C_TIMER + 6], (unsigned long long)rt1);
-      atomicAdd(&g[C_TIMER + 7], 1ull);
+      atomicAdd(&g[C_TIMER + T_RT_SUM], (unsigned long long)(rt1 - rt0));
+      atomicMax(&g[C_TIMER + T_RT_MIN], (unsigned long long)~rt0);
+      atomicMax(&g[C_TIMER + T_RT_MAX], (unsigned long long)rt1);
+      atomicAdd(&g[C_TIMER + T_WAVES], 1ull);
       const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
       if (wave < NSTAMP_WAVES) {
-        g[C_TIMER + 8 + 2 * wave] = rt0;
-        g[C_TIMER + 9 + 2 * wave] = rt1;
+        g[C_TIMER + T_STAMPS + 2 * wave] = rt0;
+        g[C_TIMER + T_STAMPS + 1 + 2 * wave] = rt1;
       }
     }
   }
@@ -453,6 +455,11 @@ struct Grp {
     if constexpr (W > 1) __syncthreads();
   }
 
+  // LDS words of the ballot exchange (xb): two alternating regions of kFuse x W words,
+  // so a region is rewritten only after the next barrier.
+  static constexpr int kFuse = 6;
+  static constexpr int kXb = 2 * kFuse * W;
+
   // Mask of the processes for which pred holds (pred is ANDed with valid).
   PSG_DEV Mask<W> ballot(bool pred) {
     const uint64_t b = __builtin_amdgcn_ballot_w64(pred) & vmask;
@@ -460,7 +467,7 @@ struct Grp {
     if constexpr (W == 1) {
       m.w[0] = b;
     } else {
-      uint64_t* s = xb + ph * W;
+      uint64_t* s = xb + ph * kFuse * W;
       ph ^= 1;
       if (lane == 0) s[wv] = b;
       __syncthreads();
@@ -468,6 +475,31 @@ struct Grp {
       for (int i = 0; i < W; ++i) m.w[i] = rfl64(s[i]);
     }
     return m;
+  }
+  // K ballots over one barrier (W > 1: one LDS exchange instead of K).
+  template <int K>
+  PSG_DEV void ballots(const bool (&pred)[K], Mask<W> (&m)[K]) {
+    static_assert(K <= kFuse, "ballots: at most kFuse predicates");
+    uint64_t b[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) b[j] = __builtin_amdgcn_ballot_w64(pred[j]) & vmask;
+    if constexpr (W == 1) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) m[j].w[0] = b[j];
+    } else {
+      uint64_t* s = xb + ph * kFuse * W;
+      ph ^= 1;
+      if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) s[j * W + wv] = b[j];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+#pragma unroll
+        for (int i = 0; i < W; ++i) m[j].w[i] = rfl64(s[j * W + i]);
+      }
+    }
   }
   PSG_DEV bool any(bool pred) { return many(ballot(pred)); }
 
@@ -589,9 +621,12 @@ PSG_DEV void lds_sync() {
 // indexed by the instance's batch row, counters are integer sums.
 // The counters live in a.counters[C_QUEUE + q*QUEUE_STRIDE], zeroed before
 // every launch together with the result counters.
+#ifndef PSG_QUEUE_CHUNK
+#define PSG_QUEUE_CHUNK 4
+#endif
 template <int W>
 struct InstanceQueue {
-  static constexpr uint64_t kChunk = W == 1 ? 4 : 1;
+  static constexpr uint64_t kChunk = W == 1 ? PSG_QUEUE_CHUNK : 1;
   static constexpr uint64_t kDone = ~0ull;
   uint64_t cur = 0, lim = 0;  // uniform: [cur, lim) is this group's current chunk
   int tries = 0;              // queues drained so far
@@ -740,33 +775,24 @@ struct Sched {
     return good;
   }
 
-  // HO(p) for this lane's process p in round k. CB = processes crashed before
-  // round k, CN = crashing in round k (uniform). The random words are drawn in
-  // one straight-line pass over the Philox calls of p's stream (no divergent
-  // word cache): word j < W*drop feeds drop mask j / drop, word W*drop + w is
-  // the crash-round survival mask of word w.
-  PSG_DEV Mask<W> ho(int k, int pid, bool good, const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CN) const {
-    if constexpr (XHO) {  // explicit: W contiguous words per process, the wave reads 512*W contiguous bytes
-      Mask<W> m = mzero<W>();
-      if (pid < nproc) {
-        const uint64_t* q = hop + ((uint64_t)k * (uint64_t)nproc + (uint64_t)pid) * W;
-#pragma unroll
-        for (int w = 0; w < W; ++w) m.w[w] = __builtin_nontemporal_load(q + w) & full.w[w];
-      }
-      return m;
-    }
+  // Raw random words of HO(pid) in round k, drawn in one straight-line pass over
+  // the Philox calls of pid's stream (no divergent word cache): word j < W*drop
+  // feeds drop mask j / drop (dm[w] = AND of word w's drop words), word W*drop + w
+  // is the crash-round survival mask hf[w] of word w. good: the drop words are not
+  // needed (the round's common set replaces them); crash = false: the survival
+  // words are not needed (no process crashes in round k) and hf stays all-ones.
+  PSG_DEV void draw(uint32_t k, uint32_t pid, bool good, bool crash, uint64_t (&dm)[W], uint64_t (&hf)[W]) const {
     const uint32_t nd = (uint32_t)W * drop;
     const uint32_t j0 = good ? nd : 0u;
-    const uint32_t j1 = crash_on ? nd + (uint32_t)W : (good ? 0u : nd);
-    uint64_t dm[W], hf[W];
+    const uint32_t j1 = crash ? nd + (uint32_t)W : (good ? 0u : nd);
 #pragma unroll
     for (int w = 0; w < W; ++w) {
       dm[w] = ~0ull;
       hf[w] = ~0ull;
     }
     for (uint32_t sidx = j0 >> 1; 2 * sidx < j1; ++sidx) {
-      const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), (uint32_t)k, (uint32_t)pid + (sidx << 16),
-                            (uint32_t)seed, (uint32_t)(seed >> 32));
+      const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), k, pid + (sidx << 16), (uint32_t)seed,
+                            (uint32_t)(seed >> 32));
       const uint64_t wlo = (uint64_t)o.x | ((uint64_t)o.y << 32);
       const uint64_t whi = (uint64_t)o.z | ((uint64_t)o.w << 32);
 #pragma unroll
@@ -786,6 +812,12 @@ struct Sched {
         }
       }
     }
+  }
+
+  // HO(pid) from its raw words. CB = processes crashed before round k, CN =
+  // crashing in round k (uniform).
+  PSG_DEV Mask<W> assemble(int pid, bool good, const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CN,
+                           const uint64_t (&dm)[W], const uint64_t (&hf)[W]) const {
     Mask<W> base;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
@@ -795,6 +827,22 @@ struct Sched {
     if (self_bit) mset(base, pid);
     if (ho_min >= 0 && mpopc(base) <= ho_min) base = full;
     return base;
+  }
+
+  // HO(p) for this lane's process p in round k.
+  PSG_DEV Mask<W> ho(int k, int pid, bool good, const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CN) const {
+    if constexpr (XHO) {  // explicit: W contiguous words per process, the wave reads 512*W contiguous bytes
+      Mask<W> m = mzero<W>();
+      if (pid < nproc) {
+        const uint64_t* q = hop + ((uint64_t)k * (uint64_t)nproc + (uint64_t)pid) * W;
+#pragma unroll
+        for (int w = 0; w < W; ++w) m.w[w] = __builtin_nontemporal_load(q + w) & full.w[w];
+      }
+      return m;
+    }
+    uint64_t dm[W], hf[W];
+    draw((uint32_t)k, (uint32_t)pid, good, crash_on && many(CN), dm, hf);
+    return assemble(pid, good, goodS, CB, CN, dm, hf);
   }
 };
 
@@ -1145,15 +1193,19 @@ PSG_DEV int32_t maxby_ts_x(Grp<W>& g, const int32_t* xs, const Mask<W>& Mc, int 
 template <int W>
 PSG_DEV void kagree_check(Grp<W>& g, Checks& ck, int c, int kk, const Mask<W>& full, bool decided, int32_t decision,
                           const X0Set<W>& X0, bool crashed, const int32_t* dstaged) {
-  Mask<W> Y = g.ballot(decided && !crashed);
+  // decided, decided by a correct process, decided a non-initial value: one exchange
+  const bool pr[3] = {decided, decided && !crashed, decided && !X0.contains(decision)};
+  Mask<W> m[3];
+  g.template ballots<3>(pr, m);
+  Mask<W> Y = m[1];
   int distinct = 0;
   while (many(Y) && distinct <= kk) {
     const int32_t dv = g.bcast(decision, dstaged, mfirst(Y));
     Y = mandn(Y, g.ballot(decided && !crashed && decision == dv));
     ++distinct;
   }
-  const bool valid = !g.any(decided && !X0.contains(decision));
-  ck.record(fbit(distinct <= kk, 0) | fbit(valid, 1), meq(g.ballot(decided), full), c, g.lane);
+  const bool valid = !many(m[2]);
+  ck.record(fbit(distinct <= kk, 0) | fbit(valid, 1), meq(m[0], full), c, g.lane);
 }
 
 

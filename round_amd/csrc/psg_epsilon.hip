@@ -68,7 +68,7 @@ PSG_DEV void eps_check(Grp<W>& g, Checks& ck, int c, const Mask<W>& full, bool d
 template <int W, bool XHO>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a) {
   __shared__ BlockCounters bc;
-  __shared__ uint64_t xb[2 * W];
+  __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int64_t red[2 * W];
   __shared__ EpsLds<W> L;
   counters_init(&bc);

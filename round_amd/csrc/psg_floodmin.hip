@@ -22,7 +22,7 @@ struct FmLds {
 template <int W, bool XHO, class SH = NoHook>
 PSG_DEV void floodmin_body(const KArgs& a) {
   __shared__ BlockCounters bc;
-  __shared__ uint64_t xb[2 * W];
+  __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int64_t red[2 * W];
   __shared__ FmLds<W> L;
   __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
@@ -35,6 +35,8 @@ PSG_DEV void floodmin_body(const KArgs& a) {
   const int f = a.param;
   const Mask<W> full = mfull<W>(n);
 
+  PhaseTimers pt;  // profiling builds only: t0 setup, t1 HO sets, t2 update, t3 finish, t4 check, t5 frozen round
+  pt.start();
   InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
   for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
@@ -64,6 +66,7 @@ PSG_DEV void floodmin_body(const KArgs& a) {
       emit_state<W, SH>(sh, g, a, i, c, x, decided ? 1 : 0, decision, 0, 0, 0, 0, 0, hs);
     };
     if (tracing<SH>(a)) trace(0, n);
+    pt.mark(0);
     for (int k = 0; k < a.R; ++k) {
       const Mask<W> act = g.ballot(!halted);
       int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
@@ -76,6 +79,7 @@ PSG_DEV void floodmin_body(const KArgs& a) {
           CN = g.ballot(sc.crash_round == k);
         }
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+        pt.mark(1);
         if (tracing<SH>(a) && !halted) hs = mpopc(M);
         // x = min(x, min{x_q : q in M}) by ascending distinct sender values
         bool unres = !halted;
@@ -107,11 +111,15 @@ PSG_DEV void floodmin_body(const KArgs& a) {
           }
         }
       }
+      pt.mark(2);
       if constexpr (!SH::kFused) check(k + 1);
       if (tracing<SH>(a)) trace(k + 1, hs);
+      pt.mark(many(act) ? 4 : 5);
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 2, dec_val, dec_round, halt_round, x, &bc);
+    pt.mark(3);
   }
+  pt.flush(a.counters, threadIdx.x & 63);
   __syncthreads();
   counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 2, a.R);
 }

@@ -21,9 +21,12 @@ struct KsLds {
   int32_t ds[G][64 * W];       // staged decisions (spec)
 };
 
-// pick(t) = t.values.min over the staged initial values
+// pick(t) = t.values.min over the staged initial values. Fast path: if t holds
+// an origin of the instance's smallest initial value xmin (Emin = those origins,
+// uniform), that is the min; otherwise walk t.
 template <int W>
-PSG_DEV int32_t kset_pick(const Mask<W>& t, const int32_t* x0s) {
+PSG_DEV int32_t kset_pick(const Mask<W>& t, const int32_t* x0s, const Mask<W>& Emin, int32_t xmin) {
+  if (many(mand(t, Emin))) return xmin;
   int32_t m = INT32_MAX;
 #pragma unroll
   for (int w = 0; w < W; ++w) {
@@ -50,7 +53,7 @@ PSG_DEV Mask<W> load_t(const uint64_t* ts, int q) {
 template <int W, bool XHO, class SH = NoHook>
 PSG_DEV void kset_body(const KArgs& a) {
   __shared__ BlockCounters bc;
-  __shared__ uint64_t xb[2 * W];
+  __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int64_t red[2 * W];
   __shared__ KsLds<W> L;
   __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
@@ -67,6 +70,8 @@ PSG_DEV void kset_body(const KArgs& a) {
   int32_t* x0s = L.x0s[grp];
   int32_t* ds = L.ds[grp];
 
+  PhaseTimers pt;  // profiling builds only: t0 setup, t1 HO sets, t2 update, t3 finish, t4 check, t5 frozen round
+  pt.start();
   InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
   for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
@@ -79,6 +84,8 @@ PSG_DEV void kset_body(const KArgs& a) {
     x0s[g.pid] = x0;
     X0Set<W> X0;
     X0.build(g, x0tab[grp], x0);
+    const int32_t xmin = g.min32(x0, true);
+    const Mask<W> Emin = g.ballot(x0 == xmin);
     // t = Map(id -> io.initialValue); decider = false (KSetAgreement.scala:27-31)
     Mask<W> t = mzero<W>();
     if (g.valid) mset(t, g.pid);
@@ -94,9 +101,10 @@ PSG_DEV void kset_body(const KArgs& a) {
     };
     if constexpr (!SH::kFused) check(0);
     auto trace = [&](int c, int32_t hs) {
-      emit_state<W, SH>(sh, g, a, i, c, kset_pick<W>(t, x0s), decided ? 1 : 0, decision, 0, 0, 0, 0, 0, hs);
+      emit_state<W, SH>(sh, g, a, i, c, kset_pick<W>(t, x0s, Emin, xmin), decided ? 1 : 0, decision, 0, 0, 0, 0, 0, hs);
     };
     if (tracing<SH>(a)) trace(0, n);
+    pt.mark(0);
     for (int k = 0; k < a.R; ++k) {
       const Mask<W> act = g.ballot(!halted);
       int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
@@ -109,6 +117,7 @@ PSG_DEV void kset_body(const KArgs& a) {
           CN = g.ballot(sc.crash_round == k);
         }
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+        pt.mark(1);
         if (tracing<SH>(a) && !halted) hs = mpopc(M);
         const Mask<W> Dm = mand(g.ballot(decider), act);  // senders' decider flags (pre-state)
 #pragma unroll
@@ -121,12 +130,34 @@ PSG_DEV void kset_body(const KArgs& a) {
         Mask<W> tnew = t;
         bool becomeDecider = false;
         if (g.any(mergep)) {
-          // same = mailbox.filter(_._2._2 == t); union of all received t
+          // same = mailbox.filter(_._2._2 == t).size; uni = t ++ every received t. The alive
+          // senders are taken class by class (equal t, one ballot per class: a class's t is
+          // read once, and same = |M & class of t|), at most kClasses classes; senders left
+          // after that are walked one by one. Round 0 (every alive sender still holds only
+          // its own origin) is closed form: same = [p in M], uni = t | M.
+          constexpr int kClasses = 8;
           int same = 0;
           Mask<W> uni = t;
+          Mask<W> rem = act;
+          Mask<W> own = mzero<W>();
+          if (g.valid) mset(own, g.pid);
+          if (!many(mand(act, g.ballot(!meq(t, own))))) {
+            same = mtest(M, g.pid) ? 1 : 0;
+            uni = mor(t, M);
+            rem = mzero<W>();
+          }
+          for (int cls = 0; cls < kClasses && many(rem); ++cls) {
+            const Mask<W> tq = load_t<W>(ts, mfirst(rem));
+            const bool mine = meq(t, tq);
+            const Mask<W> E = mand(g.ballot(mine), rem);
+            rem = mandn(rem, E);
+            const Mask<W> ME = mand(M, E);
+            if (mine) same = mpopc(ME);
+            if (many(ME)) uni = mor(uni, tq);
+          }
 #pragma unroll
           for (int w = 0; w < W; ++w) {
-            uint64_t m = act.w[w];
+            uint64_t m = rem.w[w];
             while (m) {
               const int q = w * 64 + __builtin_ctzll(m);
               m &= m - 1;
@@ -189,7 +220,7 @@ PSG_DEV void kset_body(const KArgs& a) {
           becomeDecider = true;
         }
         if (!halted && isDec) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:119-121)
-          const int32_t v = kset_pick<W>(t, x0s);
+          const int32_t v = kset_pick<W>(t, x0s, Emin, xmin);
           dec_val = v;
           dec_round = k;
           decided = true;
@@ -203,13 +234,17 @@ PSG_DEV void kset_body(const KArgs& a) {
         }
         if (halt_round == k) halted = true;
       }
+      pt.mark(2);
       if constexpr (!SH::kFused) check(k + 1);
       if (tracing<SH>(a)) trace(k + 1, hs);
+      pt.mark(many(act) ? 4 : 5);
     }
-    const int32_t mainx = g.valid ? kset_pick<W>(t, x0s) : 0;
+    const int32_t mainx = g.valid ? kset_pick<W>(t, x0s, Emin, xmin) : 0;
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 2, dec_val, dec_round, halt_round, mainx, &bc);
     lds_sync<W>();
+    pt.mark(3);
   }
+  pt.flush(a.counters, threadIdx.x & 63);
   __syncthreads();
   counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 2, a.R);
 }

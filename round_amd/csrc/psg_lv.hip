@@ -67,22 +67,33 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, const X0Set<W>& X0, Checks& ck, in
   const bool c5 = mtest(C, coord) || !g.any(ts == r4);  // (i.ts == r/4) ==> coord.commit
   bool maj = false;
   if (c > 0 && zOk && c5) {
-    // exists t: A = {i : i.ts >= t}, |A| > n/2, t <= r/4, all x over A equal (to the pinned value)
-    auto tryT = [&](int32_t t) {
-      const Mask<W> A = g.ballot(ts >= t);
-      if (mpopc(A) > n / 2 && t <= r4) {
-        const int32_t xv = g.bcast(x, L.xs, mfirst(A));
-        const bool allSame = !many(mand(A, g.ballot(x != xv)));
-        if (allSame && (!zAny || xv == z0)) maj = true;
+    // exists t <= r/4: A_t = {i : i.ts >= t}, |A_t| > n/2, all x over A_t equal (to the pinned
+    // value). The sets A_t shrink as t grows, and "all x over A equal (to z0)" holds on every
+    // non-empty subset of a set it holds on, so the exists holds iff it holds at the largest
+    // t <= r/4 with |A_t| > n/2: the (n/2+1)-th largest min(ts, r/4). Scan the distinct values
+    // of min(ts, r/4) from the top (max by ballot descent over the bits of ts+1 in [0, r/4+1])
+    // until the count passes n/2.
+    const int32_t tsc = ts < r4 ? ts : r4;
+    const uint32_t tv = (uint32_t)(tsc + 1);  // ts >= -1 (LastVoting.scala:87)
+    const int bits = 32 - __builtin_clz((uint32_t)(r4 + 1) | 1u);
+    Mask<W> below = full;  // processes under every value scanned so far
+    Mask<W> A;
+    for (;;) {
+      Mask<W> cand = below;
+      uint32_t u = 0;
+      for (int b = bits - 1; b >= 0; --b) {
+        const Mask<W> m = mand(cand, g.ballot((tv >> b) & 1u));
+        if (many(m)) {
+          cand = m;
+          u |= 1u << b;
+        }
       }
-    };
-    tryT(INT32_MIN);
-    Mask<W> rem = full;
-    while (!maj && many(rem)) {
-      const int32_t u = g.bcast(ts, L.tss, mfirst(rem));
-      rem = mandn(rem, g.ballot(ts == u));
-      tryT(u + 1);
+      A = g.ballot(tv >= u);
+      if (mpopc(A) > n / 2) break;
+      below = mandn(full, A);
     }
+    const int32_t xv = g.bcast(x, L.xs, mfirst(A));
+    maj = !many(mand(A, g.ballot(x != xv))) && (!zAny || xv == z0);
   }
   const bool inv0 = keep && (noDec || maj);
   const bool validity = X0.all_in(g, D, decision);
@@ -114,12 +125,44 @@ PSG_DEV Mask<W> ho_of(Grp<W>& g, LvLds<W>& L, const Mask<W>& ho, int c) {
   return m;
 }
 
+// R0 and R2 read only the coordinator's HO set (LastVoting.scala:118-135, 166-180).
+// Rather than every lane drawing its own HO set in those rounds, lane l draws the
+// raw words of the coordinator of the l-th such round (q = l: k = 4*(q/2) + 2*(q%2),
+// coord = (k/4) % n), one vector pass of Philox calls per 64 coordinator rounds;
+// round k assembles HO(coord) from a readlane of them (Sched::draw / assemble, the
+// same words and the same assembly as a per-lane Sched::ho).
+template <int W, bool XHO>
+struct CoordWords {
+  uint64_t dm[W], hf[W];
+  int qbase;
+  PSG_DEV static int index(int k) { return (k >> 2) * 2 + ((k >> 1) & 1); }  // k even
+  PSG_DEV void prep(const Sched<W, XHO>& sc, int q0, int lane, int n) {
+    qbase = q0;
+    const int q = q0 + lane;
+    const int k = 4 * (q >> 1) + 2 * (q & 1);
+    sc.draw((uint32_t)k, (uint32_t)((k >> 2) % n), false, sc.crash_on, dm, hf);
+  }
+  PSG_DEV Mask<W> ho(const Sched<W, XHO>& sc, int k, int c, int lane, int n, bool good, const Mask<W>& goodS,
+                     const Mask<W>& CB, const Mask<W>& CN) {
+    const int q = index(k);
+    if (q - qbase >= 64) prep(sc, q, lane, n);
+    const int off = q - qbase;
+    uint64_t d[W], h[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      d[w] = readlane64(dm[w], off);
+      h[w] = readlane64(hf[w], off);
+    }
+    return sc.assemble(c, good, goodS, CB, CN, d, h);
+  }
+};
+
 // Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
 // fused Spec module (round_amd/formula.py compile_native(fused=True)).
 template <int W, bool XHO, class SH = NoHook>
 PSG_DEV void lv_body(const KArgs& a) {
   __shared__ BlockCounters bc;
-  __shared__ uint64_t xb[2 * W];
+  __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int64_t red[2 * W];
   __shared__ LvLds<W> L;
   __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
@@ -135,12 +178,16 @@ PSG_DEV void lv_body(const KArgs& a) {
   const Mask<W> full = mfull<W>(n);
   const uint32_t myh = scala_improve((uint32_t)g.pid);
 
+  PhaseTimers pt;  // profiling builds only: t0 setup, t1 HO sets, t2 update, t3 finish, t4 check, t5 frozen round
+  pt.start();
   InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
   for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
     sc.prep_good(0, g.lane, a.R);
+    CoordWords<W, XHO> cw;
+    if constexpr (!XHO) cw.prep(sc, 0, g.lane, n);
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_LAST_VOTING);
     X0Set<W> X0;
@@ -158,6 +205,7 @@ PSG_DEV void lv_body(const KArgs& a) {
                    (fl & F_COMMIT) ? 1 : 0, vote, 0, hs);
     };
     if (tracing<SH>(a)) trace(0, n);
+    pt.mark(0);
 
     for (int k = 0; k < a.R; ++k) {
       const uint32_t old_fl = fl;
@@ -176,11 +224,30 @@ PSG_DEV void lv_body(const KArgs& a) {
           CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
           CN = g.ballot(sc.crash_round == k);
         }
-        const Mask<W> HO = sc.ho(k, g.pid, good, goodS, CB, CN);
+        // R1 / R3 read bit coord of every HO(p) (a mailbox of at most the coordinator's
+        // message); R0 / R2 only HO(coord)
+        const bool coordRound = (k & 1) == 0;
+        Mask<W> HO = mzero<W>(), HOc = mzero<W>();
+        if constexpr (XHO) {
+          HO = sc.ho(k, g.pid, good, goodS, CB, CN);
+        } else if (!coordRound) {
+          // only bit coord of HO(p) is read: the crash-round survival words matter only
+          // when the coordinator crashes in this round, or when |HO(p)| decides the
+          // ho_min rule (other bits are left unspecified otherwise)
+          uint64_t dm[W], hf[W];
+          const bool crash = sc.crash_on && (mtest(CN, c) || (sc.ho_min >= 0 && many(CN)));
+          sc.draw((uint32_t)k, (uint32_t)g.pid, good, crash, dm, hf);
+          HO = sc.assemble(g.pid, good, goodS, CB, CN, dm, hf);
+        }
+        if (coordRound) {
+          if constexpr (XHO) HOc = ho_of<W>(g, L, HO, c);
+          else HOc = cw.ho(sc, k, c, g.lane, n, good, goodS, CB, CN);
+        }
+        pt.mark(1);
         lv_stage<W>(g, L, x, ts, vote, decision);
         switch (k & 3) {
           case 0: {  // R0: send (x, ts) to coord; coord picks vote = x of maxBy ts
-            const Mask<W> Mc = mand(ho_of<W>(g, L, HO, c), act);
+            const Mask<W> Mc = mand(HOc, act);
             const int size = mpopc(Mc);
             hs = g.pid == c ? size : 0;
             if (cAlive && (size > n / 2 || (k == 0 && size > 0))) {
@@ -204,7 +271,7 @@ PSG_DEV void lv_body(const KArgs& a) {
             break;
           }
           case 2: {  // R2: ts == r/4 send x to coord; coord ready on a majority
-            const Mask<W> Mc = mand(mand(ho_of<W>(g, L, HO, c), act), g.ballot(ts == phase));
+            const Mask<W> Mc = mand(mand(HOc, act), g.ballot(ts == phase));
             hs = g.pid == c ? mpopc(Mc) : 0;
             if (cAlive && mpopc(Mc) > need2 && g.pid == c) fl |= F_READY;
             break;
@@ -227,18 +294,26 @@ PSG_DEV void lv_body(const KArgs& a) {
             break;
           }
         }
+        pt.mark(2);
       }
       if constexpr (!SH::kFused) lv_check<W>(g, L, X0, ck, k + 1, true, n, full, x, ts, vote, decision, fl, old_fl, old_decision);
       if (tracing<SH>(a)) trace(k + 1, (old_fl & F_HALTED) ? n : hs);
+      pt.mark(many(act) ? 4 : 5);
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 7, dec_val, dec_round, halt_round, x, &bc);
+    pt.mark(3);
   }
+  pt.flush(a.counters, threadIdx.x & 63);
   __syncthreads();
   counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 7, a.R);
 }
 
+#ifndef PSG_LV_WPE
+#define PSG_LV_WPE 6
+#endif
 template <int W, bool XHO, class SH = NoHook>
-__global__ void __launch_bounds__(Geometry<W>::kThreads) lv_kernel(KArgs a) {
+__global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? PSG_LV_WPE : 1)))
+lv_kernel(KArgs a) {
   lv_body<W, XHO, SH>(a);
 }
 

@@ -73,7 +73,7 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
 template <int W, bool V2, bool XHO, class SH = NoHook>
 PSG_DEV void otr_body(const KArgs& a) {
   __shared__ BlockCounters bc;
-  __shared__ uint64_t xb[2 * W];
+  __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int64_t red[2 * W];
   __shared__ OtrLds<W> L;
   __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
@@ -87,7 +87,7 @@ PSG_DEV void otr_body(const KArgs& a) {
   const Mask<W> full = mfull<W>(n);
   const uint32_t valid01 = g.valid ? 1u : 0u;
 
-  PhaseTimers pt;  // profiling builds only
+  PhaseTimers pt;  // profiling builds only: t0 setup, t1 active round, t2 frozen round, t3 finish
   pt.start();
   InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
   for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
@@ -178,8 +178,11 @@ PSG_DEV void otr_body(const KArgs& a) {
   counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 8, a.R);
 }
 
+#ifndef PSG_OTR_WPE
+#define PSG_OTR_WPE 6
+#endif
 template <int W, bool V2, bool XHO, class SH = NoHook>
-__global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? 6 : 1)))
+__global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? PSG_OTR_WPE : 1)))
 otr_kernel(KArgs a) {
   otr_body<W, V2, XHO, SH>(a);
 }

@@ -16,7 +16,7 @@ namespace psg {
 
 template <int W>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) schedule_kernel(KArgs a, uint64_t* ho_out, int32_t* crash_out) {
-  __shared__ uint64_t xb[2 * W];
+  __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int64_t red[2 * W];
   Grp<W> g;
   grp_setup(g, a, xb, red);

@@ -56,7 +56,7 @@ PSG_DEV Mask<W> slv_ho_of(Grp<W>& g, SlvLds<W>& L, const Mask<W>& ho, int c) {
 template <int W, bool XHO, class SH = NoHook>
 PSG_DEV void slv_body(const KArgs& a) {
   __shared__ BlockCounters bc;
-  __shared__ uint64_t xb[2 * W];
+  __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int64_t red[2 * W];
   __shared__ SlvLds<W> L;
   __shared__ ChampTable<W> CT;

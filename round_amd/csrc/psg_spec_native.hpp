@@ -323,7 +323,7 @@ PSG_DEV int32_t imul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uin
 template <int W, class S>
 __device__ void native_kernel_body(const VmArgs& A) {
   __shared__ BlockCounters bc;
-  __shared__ uint64_t xb[2 * W];
+  __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int64_t red[2 * W];
   __shared__ int32_t stg[W > 1 ? 3 * PSG_NFIELDS * 64 * W : 1];
   __shared__ int32_t scratch[Geometry<W>::kGroups][64 * W];

@@ -1,4 +1,4 @@
-"""A/B probe of the headline launch (OTR n=64, 1e7 instances, R=20, V=64 and V=2):
+"""A/B probe of the headline launch (OTR n=64, 1e7 instances, R=20, V=64 and V=2; arg lv: C3 LastVoting):
 min kernel ms over 5 launches for the library PSG_LIB points at (default: in-tree)."""
 import os
 import sys
@@ -6,12 +6,16 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from round_amd import lib, psync  # noqa: E402
 
-I = 10_000_000
-for V in (64, 2):
-    with psync.GpuRound(psync.OTR(), 64, 20, seed=2, value_range=V, batch_capacity=I) as g:
+which = sys.argv[1] if len(sys.argv) > 1 else "otr"
+if which == "otr":
+    runs = [(psync.OTR(), 10_000_000, dict(value_range=V), f"V={V}") for V in (64, 2)]
+else:  # BASELINE C3 shard: LastVoting n=64, 1.25e7 instances, crash-stop
+    runs = [(psync.LastVoting(), 12_500_000, {}, "LV C3")]
+for alg, I, kw, label in runs:
+    with psync.GpuRound(alg, 64, 20, seed=2, batch_capacity=I, **kw) as g:
         g.load_inputs(0, I)
         g.run(0, I)
         ks = [g.run(0, I).summary.kernel_ns / 1e6 for _ in range(5)]
         d = g.run(0, I).summary.digest
-    print(f"{os.path.basename(os.path.dirname(os.path.dirname(lib.LIB_PATH)))} V={V}: {min(ks):.2f} ms digest {d}",
+    print(f"{os.path.basename(os.path.dirname(os.path.dirname(lib.LIB_PATH)))} {label}: {min(ks):.2f} ms digest {d}",
           flush=True)
