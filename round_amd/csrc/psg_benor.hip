@@ -45,6 +45,7 @@ template <int W, bool XHO, class SH = NoHook>
 PSG_DEV void benor_body(const KArgs& a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[Grp<W>::kXb];
+  __shared__ int32_t crl[W > 1 ? 64 * W : 1];
   __shared__ int64_t red[2 * W];
   counters_init(&bc);
   __syncthreads();
@@ -60,6 +61,8 @@ PSG_DEV void benor_body(const KArgs& a) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
+    CrashSets<W> cs;  // per-instance crash rounds (no per-round exchange for W > 1)
+    if (sc.crash_on) cs.prep(g, crl, sc.crash_round);
     sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_BENOR);
@@ -86,10 +89,7 @@ PSG_DEV void benor_body(const KArgs& a) {
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
-        if (sc.crash_on) {
-          CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
-          CN = g.ballot(sc.crash_round == k);
-        }
+        if (sc.crash_on) cs.sets(g, k, CB, CN);
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const int size = mpopc(M);
         if (!halted) hs = size;

@@ -586,6 +586,31 @@ struct Grp {
     if constexpr (W == 1) return m;
     else return (int32_t)cross64<0>(m);
   }
+  // min32 over the `in` lanes and the group OR of `flag` in one exchange
+  PSG_DEV int32_t min32_any(int32_t v, bool in, bool flag, bool& any) {
+    const int32_t m = wave_min32((in && valid) ? v : INT32_MAX);
+    const bool f = (__builtin_amdgcn_ballot_w64(flag) & vmask) != 0ull;
+    if constexpr (W == 1) {
+      any = f;
+      return m;
+    } else {
+      int64_t* s = red + ph * W;
+      ph ^= 1;
+      if (lane == 0) s[wv] = ((int64_t)(f ? 1 : 0) << 32) | (int64_t)(uint32_t)m;
+      __syncthreads();
+      int32_t r = INT32_MAX;
+      bool a = false;
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        const int64_t t = s[i];
+        const int32_t ti = (int32_t)(uint32_t)t;
+        r = ti < r ? ti : r;
+        a = a || (t >> 32) != 0;
+      }
+      any = a;
+      return r;
+    }
+  }
   PSG_DEV int32_t max32(int32_t v, bool in) {
     int32_t m = wave_max32((in && valid) ? v : INT32_MIN);
     if constexpr (W == 1) return m;
@@ -843,6 +868,40 @@ struct Sched {
     uint64_t dm[W], hf[W];
     draw((uint32_t)k, (uint32_t)pid, good, crash_on && many(CN), dm, hf);
     return assemble(pid, good, goodS, CB, CN, dm, hf);
+  }
+};
+
+// Crash sets of round k: CB = processes crashed before round k, CN = crashing in
+// round k. A process's crash round is fixed per instance, so for W > 1 the
+// instance's crash rounds are staged in LDS once (one barrier per instance) and
+// lane l keeps those of processes w*64 + l in registers: every wave then forms
+// CB(k) / CN(k) from 2W local ballots, with no per-round cross-wave exchange.
+// W == 1: the two ballots are already wave-local.
+template <int W>
+struct CrashSets {
+  int32_t cr[W];
+  // lds: 64*W words (W > 1); call from uniform control flow (block barrier)
+  PSG_DEV void prep(Grp<W>& g, int32_t* lds, int32_t my_crash_round) {
+    if constexpr (W == 1) {
+      cr[0] = my_crash_round;
+    } else {
+      lds[g.pid] = g.valid ? my_crash_round : -1;
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < W; ++w) cr[w] = lds[w * 64 + g.lane];
+    }
+  }
+  PSG_DEV void sets(Grp<W>& g, int k, Mask<W>& CB, Mask<W>& CN) const {
+    if constexpr (W == 1) {
+      CB = g.ballot(cr[0] >= 0 && cr[0] < k);
+      CN = g.ballot(cr[0] == k);
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        CB.w[w] = __builtin_amdgcn_ballot_w64(cr[w] >= 0 && cr[w] < k);
+        CN.w[w] = __builtin_amdgcn_ballot_w64(cr[w] == k);
+      }
+    }
   }
 };
 

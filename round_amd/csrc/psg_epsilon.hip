@@ -69,6 +69,7 @@ template <int W, bool XHO>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[Grp<W>::kXb];
+  __shared__ int32_t crl[W > 1 ? 64 * W : 1];
   __shared__ int64_t red[2 * W];
   __shared__ EpsLds<W> L;
   counters_init(&bc);
@@ -91,6 +92,8 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a)
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
+    CrashSets<W> cs;  // per-instance crash rounds (no per-round exchange for W > 1)
+    if (sc.crash_on) cs.prep(g, crl, sc.crash_round);
     sc.prep_good(0, g.lane, a.R);
     double x0 = 0.0;
     if (g.valid) {
@@ -122,10 +125,7 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a)
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
-        if (sc.crash_on) {
-          CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
-          CN = g.ballot(sc.crash_round == k);
-        }
+        if (sc.crash_on) cs.sets(g, k, CB, CN);
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const Mask<W> Fl = mand(g.ballot(!(k <= maxR)), act);  // senders announcing their halt
         const Mask<W> U = mor(M, H);                             // V = mailbox ++ halted.values

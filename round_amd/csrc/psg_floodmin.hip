@@ -23,6 +23,7 @@ template <int W, bool XHO, class SH = NoHook>
 PSG_DEV void floodmin_body(const KArgs& a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[Grp<W>::kXb];
+  __shared__ int32_t crl[W > 1 ? 64 * W : 1];
   __shared__ int64_t red[2 * W];
   __shared__ FmLds<W> L;
   __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
@@ -42,6 +43,8 @@ PSG_DEV void floodmin_body(const KArgs& a) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
+    CrashSets<W> cs;  // per-instance crash rounds (no per-round exchange for W > 1)
+    if (sc.crash_on) cs.prep(g, crl, sc.crash_round);
     sc.prep_good(0, g.lane, a.R);
     const bool crashed = sc.crash_round >= 0;
     int32_t x0 = 0;
@@ -74,20 +77,24 @@ PSG_DEV void floodmin_body(const KArgs& a) {
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
-        if (sc.crash_on) {
-          CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
-          CN = g.ballot(sc.crash_round == k);
-        }
+        if (sc.crash_on) cs.sets(g, k, CB, CN);
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         pt.mark(1);
         if (tracing<SH>(a) && !halted) hs = mpopc(M);
         // x = min(x, min{x_q : q in M}) by ascending distinct sender values
+        // (W > 1: the min and "any lane unresolved" share one exchange, E and "any lane
+        // still below v" share another; a converged round costs two exchanges)
         bool unres = !halted;
         int32_t nx = x;
         Mask<W> rem = act;
-        while (many(rem) && g.any(unres)) {
-          const int32_t v = g.min32(x, mtest(rem, g.pid));  // rem non-empty: v is a sender value
-          const Mask<W> E = mand(g.ballot(x == v), rem);
+        while (many(rem)) {
+          bool anyU;
+          const int32_t v = g.min32_any(x, mtest(rem, g.pid), unres, anyU);  // rem non-empty: a sender value
+          if (!anyU) break;
+          const bool pr[2] = {x == v, unres && v < x};
+          Mask<W> m2[2];
+          g.template ballots<2>(pr, m2);
+          const Mask<W> E = mand(m2[0], rem);
           rem = mandn(rem, E);
           if (unres) {
             if (v >= x) {
@@ -97,6 +104,7 @@ PSG_DEV void floodmin_body(const KArgs& a) {
               unres = false;
             }
           }
+          if (!many(m2[1])) break;  // every unresolved lane had v >= x: all resolved
         }
         if (!halted) {
           x = nx;

@@ -25,6 +25,7 @@ template <int W, bool XHO, class SH = NoHook>
 PSG_DEV void kset_es_body(const KArgs& a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[Grp<W>::kXb];
+  __shared__ int32_t crl[W > 1 ? 64 * W : 1];
   __shared__ int64_t red[2 * W];
   __shared__ EsLds<W> L;
   __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
@@ -42,6 +43,8 @@ PSG_DEV void kset_es_body(const KArgs& a) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
+    CrashSets<W> cs;  // per-instance crash rounds (no per-round exchange for W > 1)
+    if (sc.crash_on) cs.prep(g, crl, sc.crash_round);
     sc.prep_good(0, g.lane, a.R);
     const bool crashed = sc.crash_round >= 0;
     int32_t x0 = 0;
@@ -68,28 +71,31 @@ PSG_DEV void kset_es_body(const KArgs& a) {
     };
     if (tracing<SH>(a)) trace(0, n);
     for (int k = 0; k < a.R; ++k) {
-      const Mask<W> act = g.ballot(!halted);
+      // pre-state ballots: alive senders, senders' canDecide flags (one exchange)
+      const bool pr0[2] = {!halted, cd};
+      Mask<W> m0[2];
+      g.template ballots<2>(pr0, m0);
+      const Mask<W> act = m0[0];
       int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
-        if (sc.crash_on) {
-          CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
-          CN = g.ballot(sc.crash_round == k);
-        }
+        if (sc.crash_on) cs.sets(g, k, CB, CN);
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const int currNb = mpopc(M);
         if (!halted) hs = currNb;
-        const bool anyCD = many(mand(M, g.ballot(cd)));  // mailbox.exists(_._2._2), pre-update flags
+        const bool anyCD = many(mand(M, m0[1]));  // mailbox.exists(_._2._2), pre-update flags
         const bool decideNow = !halted && (k > t / kk || cd);
         // est = min over the mailbox's estimates (unchanged if the mailbox is empty)
         bool unres = !halted && !decideNow && currNb > 0;
         const bool selfIn = mtest(M, g.pid);
         int32_t nest = est;
         Mask<W> rem = act;
-        while (many(rem) && g.any(unres)) {
-          const int32_t v = g.min32(est, mtest(rem, g.pid));
+        while (many(rem)) {
+          bool anyU;  // the min and "any lane unresolved" share one exchange
+          const int32_t v = g.min32_any(est, mtest(rem, g.pid), unres, anyU);
+          if (!anyU) break;
           const Mask<W> E = mand(g.ballot(est == v), rem);
           rem = mandn(rem, E);
           if (unres) {

@@ -163,6 +163,7 @@ template <int W, bool XHO, class SH = NoHook>
 PSG_DEV void lv_body(const KArgs& a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[Grp<W>::kXb];
+  __shared__ int32_t crl[W > 1 ? 64 * W : 1];
   __shared__ int64_t red[2 * W];
   __shared__ LvLds<W> L;
   __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
@@ -185,6 +186,8 @@ PSG_DEV void lv_body(const KArgs& a) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
+    CrashSets<W> cs;  // per-instance crash rounds (no per-round exchange for W > 1)
+    if (sc.crash_on) cs.prep(g, crl, sc.crash_round);
     sc.prep_good(0, g.lane, a.R);
     CoordWords<W, XHO> cw;
     if constexpr (!XHO) cw.prep(sc, 0, g.lane, n);
@@ -220,10 +223,7 @@ PSG_DEV void lv_body(const KArgs& a) {
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
-        if (sc.crash_on) {
-          CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
-          CN = g.ballot(sc.crash_round == k);
-        }
+        if (sc.crash_on) cs.sets(g, k, CB, CN);
         // R1 / R3 read bit coord of every HO(p) (a mailbox of at most the coordinator's
         // message); R0 / R2 only HO(coord)
         const bool coordRound = (k & 1) == 0;
