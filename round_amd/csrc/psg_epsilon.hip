@@ -142,27 +142,69 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a)
           const int64_t kj = W == 1 ? (int64_t)readlane64((uint64_t)key, j) : L.keys[j];
           rank += (kj < key || (kj == key && j < g.pid)) ? 1 : 0;
         }
+        // sorted values to LDS (position = rank), then per lane: min, max, V(2f) and the
+        // trimmed every-2f-th sum over the members of its own V (Epsilon.scala:31-42)
         if (g.valid) {
           sx[rank] = x;
-          spid[rank] = g.pid;
+          if constexpr (W > 1) spid[rank] = g.pid;
         }
         lds_sync<W>();
-        // walk the sorted values keeping the members of V: min, max, V(2f) and the
-        // trimmed every-2f-th sum (Epsilon.scala:31-42)
         double first = 0.0, last = 0.0, e2f = 0.0, sum = 0.0;
-        int cnt = 0, j = 0;
-        for (int t = 0; t < n; ++t) {
-          const int q = spid[t];
-          if (mtest(U, q)) {
-            const double v = sx[t];
-            if (j == 0) first = v;
-            last = v;
-            if (j == 2 * f) e2f = v;
-            if (j >= f && j < m - f && (j - f) % (2 * f) == 0) {
-              sum += v;
-              ++cnt;
+        int cnt = 0;
+        if constexpr (W == 1) {
+          // Us = V as a mask over sorted positions (bit t: the process at position t is in
+          // V); the pid column is a forward lane permute by rank read at uniform positions.
+          // The selected members j = f, 3f, 5f, ... < m - f are then found by dropping the
+          // lowest set bits, and only those positions are read from LDS.
+          const int spid_r = __builtin_amdgcn_ds_permute((g.valid ? rank : g.lane) << 2, g.pid);
+          uint32_t us_lo = 0, us_hi = 0;
+          const int n_lo = n < 32 ? n : 32;
+          for (int t = 0; t < n_lo; ++t) {
+            const int q = __builtin_amdgcn_readlane(spid_r, t);
+            us_lo |= (uint32_t)((U.w[0] >> q) & 1ull) << t;
+          }
+          for (int t = 32; t < n; ++t) {
+            const int q = __builtin_amdgcn_readlane(spid_r, t);
+            us_hi |= (uint32_t)((U.w[0] >> q) & 1ull) << (t - 32);
+          }
+          const uint64_t Us = ((uint64_t)us_hi << 32) | us_lo;
+          if (!halted && m > 0) {
+            if (k == 0) {
+              first = sx[__builtin_ctzll(Us)];
+              last = sx[63 - __builtin_clzll(Us)];
+              if (m > 2 * f) {
+                uint64_t S = Us;
+                for (int d = 0; d < 2 * f; ++d) S &= S - 1;
+                e2f = sx[__builtin_ctzll(S)];
+              }
+            } else if (k <= maxR) {
+              uint64_t S = Us;
+              for (int d = 0; d < f; ++d) S &= S - 1;
+              for (int j = f; j < m - f; j += 2 * f) {  // ascending left fold from 0.0
+                sum += sx[__builtin_ctzll(S)];
+                ++cnt;
+                for (int d = 0; d < 2 * f; ++d) S &= S - 1;
+              }
             }
-            ++j;
+          }
+        } else {
+          // W > 1: every lane walks the sorted list once with broadcast LDS reads;
+          // the selected members are tracked with a running index (no modulo)
+          int j = 0, nsel = f;
+          const int jhi = m - f;
+          for (int t = 0; t < n; ++t) {
+            if (mtest(U, spid[t])) {
+              const double v = sx[t];
+              if (j == 0) first = v;
+              last = v;
+              if (j == 2 * f) e2f = v;
+              if (j == nsel && j < jhi) {
+                sum += v;
+                ++cnt;
+                nsel += 2 * f;
+              }
+              ++j;
+            }
           }
         }
         if (!halted) {
