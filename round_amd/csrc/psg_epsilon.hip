@@ -48,6 +48,24 @@ struct EpsLds {
   int64_t keys[W > 1 ? 64 * W : 1];
 };
 
+// Ascending bitonic sort of (key, pid) pairs over the 64 lanes of a wave (pairs must
+// be distinct; pids are). Stage (size, d): partners lane ^ d exchange through the LDS
+// crossbar; the lower lane of a pair keeps the smaller pair in an ascending block.
+PSG_DEV void wave_sort_key_pid(int64_t& key, int32_t& pid, int lane) {
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int d = size >> 1; d > 0; d >>= 1) {
+      const int64_t pk = __shfl_xor(key, d);
+      const int32_t pp = __shfl_xor(pid, d);
+      const bool less = pk < key || (pk == key && pp < pid);  // partner's pair precedes mine
+      const bool take = less != (((lane & d) != 0) != ((lane & size) != 0));
+      key = take ? pk : key;
+      pid = take ? pp : pid;
+    }
+  }
+}
+
 // Slots: 0 EpsAgreement (no NaN decision, max - min <= eps), 1 EpsValidity (every
 // decision within [min, max] of the non-NaN initial values), 2 SafetyPredicate
 // (|V| >= n - f for every process that took a step). Termination: all decided.
@@ -131,32 +149,40 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a)
         const Mask<W> U = mor(M, H);                             // V = mailbox ++ halted.values
         const int m = mpopc(U);
         pred = !g.any(!halted && m < n - f);
-        // rank every process's current x in total order (ties by pid), scatter to LDS
+        // sort every process's current x in total order (ties by pid): W = 1 a wave bitonic
+        // network over (key, pid) pairs, lane t ends with the t-th pair; W > 1 a rank count
+        // over the keys staged in LDS. Sorted values go to LDS (position = rank).
         const int64_t key = total_key(x);
-        int rank = 0;
-        if constexpr (W > 1) {
+        int32_t spid_r = 0;  // W = 1: pid at sorted position = lane
+        if constexpr (W == 1) {
+          int64_t skey = g.valid ? key : INT64_MAX;  // padding lanes sort last
+          spid_r = g.lane;
+          wave_sort_key_pid(skey, spid_r, g.lane);
+          const double xs = __shfl(x, spid_r);
+          if (g.lane < n) sx[g.lane] = xs;
+        } else {
           L.keys[g.pid] = key;
           __syncthreads();
-        }
-        for (int j = 0; j < n; ++j) {
-          const int64_t kj = W == 1 ? (int64_t)readlane64((uint64_t)key, j) : L.keys[j];
-          rank += (kj < key || (kj == key && j < g.pid)) ? 1 : 0;
-        }
-        // sorted values to LDS (position = rank), then per lane: min, max, V(2f) and the
-        // trimmed every-2f-th sum over the members of its own V (Epsilon.scala:31-42)
-        if (g.valid) {
-          sx[rank] = x;
-          if constexpr (W > 1) spid[rank] = g.pid;
+          int rank = 0;
+          for (int j = 0; j < n; ++j) {
+            const int64_t kj = L.keys[j];
+            rank += (kj < key || (kj == key && j < g.pid)) ? 1 : 0;
+          }
+          if (g.valid) {
+            sx[rank] = x;
+            spid[rank] = g.pid;
+          }
         }
         lds_sync<W>();
+        // per lane: min, max, V(2f) and the trimmed every-2f-th sum over the members of
+        // its own V (Epsilon.scala:31-42)
         double first = 0.0, last = 0.0, e2f = 0.0, sum = 0.0;
         int cnt = 0;
         if constexpr (W == 1) {
           // Us = V as a mask over sorted positions (bit t: the process at position t is in
-          // V); the pid column is a forward lane permute by rank read at uniform positions.
-          // The selected members j = f, 3f, 5f, ... < m - f are then found by dropping the
-          // lowest set bits, and only those positions are read from LDS.
-          const int spid_r = __builtin_amdgcn_ds_permute((g.valid ? rank : g.lane) << 2, g.pid);
+          // V), from the sorted pid column read at uniform positions. The selected members
+          // j = f, 3f, 5f, ... < m - f are then found by dropping the lowest set bits, and
+          // only those positions are read from LDS.
           uint32_t us_lo = 0, us_hi = 0;
           const int n_lo = n < 32 ? n : 32;
           for (int t = 0; t < n_lo; ++t) {
