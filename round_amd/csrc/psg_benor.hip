@@ -148,8 +148,12 @@ PSG_DEV void benor_body(const KArgs& a) {
   counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 5, a.R);
 }
 
+#ifndef PSG_BENOR_WPE
+#define PSG_BENOR_WPE 5  // W = 2 (C5): 5 waves/SIMD measured 1.14x over the register-bound 4
+#endif
 template <int W, bool XHO, class SH = NoHook>
-__global__ void __launch_bounds__(Geometry<W>::kThreads) benor_kernel(KArgs a) {
+__global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? 1 : PSG_BENOR_WPE)))
+benor_kernel(KArgs a) {
   benor_body<W, XHO, SH>(a);
 }
 

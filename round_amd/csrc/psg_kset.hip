@@ -249,8 +249,12 @@ PSG_DEV void kset_body(const KArgs& a) {
   counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 2, a.R);
 }
 
+#ifndef PSG_KSET_WPE
+#define PSG_KSET_WPE 4  // W = 4 (C4): 4 waves/SIMD measured 1.2x over the register-bound 3; 5 spills
+#endif
 template <int W, bool XHO, class SH = NoHook>
-__global__ void __launch_bounds__(Geometry<W>::kThreads) kset_kernel(KArgs a) {
+__global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? 1 : PSG_KSET_WPE)))
+kset_kernel(KArgs a) {
   kset_body<W, XHO, SH>(a);
 }
 
