@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--V", type=int, default=64, help="value-domain size of the headline line")
     ap.add_argument("--variants", default="2,4", help="other V values reported beside the headline")
     ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
