@@ -63,7 +63,7 @@ def pmc_traffic_bytes(args):
         if ("otr_kernel<1" in d.get("kernel", "") and "hbm" in d and w.get("n") == args.n
                 and w.get("rounds") == args.rounds and w.get("instances_per_gpu") == args.instances
                 and w.get("value_range") == args.V):
-            best = (d["hbm"]["traffic_bytes"], os.path.relpath(f, ROOT))
+            best = (d["hbm"]["traffic_bytes"], os.path.relpath(f, ROOT), d)
     return best
 
 
@@ -198,6 +198,11 @@ def main():
             out["roofline"]["traffic"] = tb[0] / head["kernel_s"] / 1e9
             out["roofline"]["traffic_bytes_per_launch"] = tb[0]
             out["roofline"]["traffic_source"] = tb[1] + " (PMC FETCH_SIZE*2 + WRITE_SIZE per launch)"
+            # the binding resource of this fused kernel is instruction issue: report the
+            # same profile's issue utilisation and per-instance-round instruction counts beside it
+            if "issue_utilization" in tb[2]:
+                out["roofline"]["issue_utilization"] = tb[2]["issue_utilization"]
+                out["roofline"]["insts_per_instance_round"] = tb[2].get("per_instance_round")
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(head["cfg"], args.cpu_seconds)
         else:

@@ -646,12 +646,15 @@ PSG_DEV void lds_sync() {
 // indexed by the instance's batch row, counters are integer sums.
 // The counters live in a.counters[C_QUEUE + q*QUEUE_STRIDE], zeroed before
 // every launch together with the result counters.
+#ifndef PSG_QUEUE_CHUNK_WIDE
+#define PSG_QUEUE_CHUNK_WIDE 4  // W > 1 (one instance per block): 1 -> 4 measured +2-4 % on C4/C5
+#endif
 #ifndef PSG_QUEUE_CHUNK
 #define PSG_QUEUE_CHUNK 4
 #endif
 template <int W>
 struct InstanceQueue {
-  static constexpr uint64_t kChunk = W == 1 ? PSG_QUEUE_CHUNK : 1;
+  static constexpr uint64_t kChunk = W == 1 ? PSG_QUEUE_CHUNK : PSG_QUEUE_CHUNK_WIDE;
   static constexpr uint64_t kDone = ~0ull;
   uint64_t cur = 0, lim = 0;  // uniform: [cur, lim) is this group's current chunk
   int tries = 0;              // queues drained so far
