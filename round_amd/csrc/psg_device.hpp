@@ -516,38 +516,47 @@ struct Grp {
     else return staged[q];
   }
 
-  // group reductions over valid lanes (inactive lanes contribute the identity)
-  PSG_DEV int64_t wave_min64(int64_t v) const {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      int64_t t = __shfl_xor(v, o);
-      v = t < v ? t : v;
-    }
-    return v;
+  // group reductions over valid lanes (inactive lanes contribute the identity).
+  // Wave part: DPP row_shr 1/2/4/8 + row_bcast 15/31 (VALU latency, no LDS-crossbar
+  // round trips), the result read from lane 63 as a uniform value; call from
+  // converged control flow (every lane of the wave active).
+  template <int CTRL, int RM>
+  PSG_DEV static int32_t dpp32(int32_t old, int32_t v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, RM, 0xF, false);
   }
-  PSG_DEV int64_t wave_max64(int64_t v) const {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      int64_t t = __shfl_xor(v, o);
-      v = t > v ? t : v;
-    }
-    return v;
+  template <int CTRL, int RM>
+  PSG_DEV static int64_t dpp64(int64_t old, int64_t v) {
+    const uint32_t lo = (uint32_t)dpp32<CTRL, RM>((int32_t)(uint32_t)old, (int32_t)(uint32_t)v);
+    const uint32_t hi = (uint32_t)dpp32<CTRL, RM>((int32_t)(old >> 32), (int32_t)(v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
   }
+  template <bool MAX>
+  PSG_DEV static int32_t dpp_reduce32(int32_t v) {
+    constexpr int32_t id = MAX ? INT32_MIN : INT32_MAX;
+#define PSG_RED32(C, R) { const int32_t t = dpp32<C, R>(id, v); v = MAX ? (t > v ? t : v) : (t < v ? t : v); }
+    PSG_RED32(0x111, 0xF) PSG_RED32(0x112, 0xF) PSG_RED32(0x114, 0xF) PSG_RED32(0x118, 0xF)
+    PSG_RED32(0x142, 0xA) PSG_RED32(0x143, 0xC)
+#undef PSG_RED32
+    return __builtin_amdgcn_readlane(v, 63);
+  }
+  template <bool MAX>
+  PSG_DEV static int64_t dpp_reduce64(int64_t v) {
+    constexpr int64_t id = MAX ? INT64_MIN : INT64_MAX;
+#define PSG_RED64(C, R) { const int64_t t = dpp64<C, R>(id, v); v = MAX ? (t > v ? t : v) : (t < v ? t : v); }
+    PSG_RED64(0x111, 0xF) PSG_RED64(0x112, 0xF) PSG_RED64(0x114, 0xF) PSG_RED64(0x118, 0xF)
+    PSG_RED64(0x142, 0xA) PSG_RED64(0x143, 0xC)
+#undef PSG_RED64
+    return (int64_t)readlane64((uint64_t)v, 63);
+  }
+  PSG_DEV int64_t wave_min64(int64_t v) const { return dpp_reduce64<false>(v); }
+  PSG_DEV int64_t wave_max64(int64_t v) const { return dpp_reduce64<true>(v); }
   PSG_DEV uint64_t wave_sum64(uint64_t v) const {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
     return v;
   }
-  PSG_DEV int32_t wave_min32(int32_t v) const {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
-    return v;
-  }
-  PSG_DEV int32_t wave_max32(int32_t v) const {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
-    return v;
-  }
+  PSG_DEV int32_t wave_min32(int32_t v) const { return dpp_reduce32<false>(v); }
+  PSG_DEV int32_t wave_max32(int32_t v) const { return dpp_reduce32<true>(v); }
   template <int OP>  // 0 min, 1 max, 2 sum, 3 or
   PSG_DEV int64_t cross64(int64_t v) {
     if constexpr (W == 1) {

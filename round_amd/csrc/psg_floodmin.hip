@@ -58,10 +58,10 @@ PSG_DEV void floodmin_body(const KArgs& a) {
     ck.reset();
     typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
     auto check = [&](int c) {
-      if constexpr (W > 1) {
-        L.ds[g.pid] = decision;
-        __syncthreads();
-      }
+      // W > 1: the staged decisions are published by the barrier of kagree_check's
+      // first ballot exchange (read only after it); the previous check's reads are
+      // ordered before this write by the next round's `act` exchange
+      if constexpr (W > 1) L.ds[g.pid] = decision;
       kagree_check<W>(g, ck, c, 1, full, decided, decision, X0, crashed, L.ds);
     };
     if constexpr (!SH::kFused) check(0);

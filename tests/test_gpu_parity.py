@@ -251,15 +251,18 @@ def test_gpu_epsilon_matches_oracle(cid, alg, n, count, kw, oracle_mod):
             assert _close(fdec[j * n + p], odec[i * n + p]) and _close(ffx[j * n + p], ofx[i * n + p]), (inst, p)
 
 
-def test_gpu_epsilon_host_inputs(oracle_mod):
-    """psg_load_inputs_f64: caller Doubles incl. negatives, -0.0 / 0.0, duplicates and NaN."""
+@pytest.mark.parametrize("n,f,dup", [(16, 2, 0.3), (33, 3, 0.6), (64, 5, 0.9)])
+def test_gpu_epsilon_host_inputs(n, f, dup, oracle_mod):
+    """psg_load_inputs_f64: caller Doubles incl. negatives, -0.0 / 0.0, duplicates and NaN.
+    n = 33 crosses the 32-position halves of the sorted-membership mask; n = 64 with 90 %
+    pooled values is tie-heavy (equal sort keys ordered by pid in the bitonic network)."""
     import random
-    rng = random.Random(9)
-    n, count = 16, 400
+    rng = random.Random(9 + n)
+    count = 400
     pool = [0.0, -0.0, 1.0, -1.0, 0.5, 0.5, 1e-300, -1e300, float("nan")]
-    init = [[rng.choice(pool) if rng.random() < 0.3 else rng.uniform(-5, 5) for _ in range(n)]
+    init = [[rng.choice(pool) if rng.random() < dup else rng.uniform(-5, 5) for _ in range(n)]
             for _ in range(count)]
-    with psync.GpuRound(psync.EpsilonConsensus(2, 1e-3), n, seed=70, batch_capacity=count) as gr:
+    with psync.GpuRound(psync.EpsilonConsensus(f, 1e-3), n, seed=70, batch_capacity=count) as gr:
         gr.load_inputs(5, count, init)
         res = gr.run(5, count, per_instance=True)
         dec, dround = gr.decisions()
