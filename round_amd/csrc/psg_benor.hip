@@ -17,20 +17,27 @@ namespace psg {
 template <int W>
 PSG_DEV void benor_check(Grp<W>& g, Checks& ck, int c, bool has_old, int n, const Mask<W>& full, bool x, bool cd,
                          int vote, bool decided, bool decision, bool old_decided, bool old_decision, bool pred) {
-  const bool noDec = !g.any(decided || cd);
-  const int cntT = mpopc(g.ballot(x));
+  // every quantified witness in two ballot exchanges (W > 1: two LDS barriers instead
+  // of one per P.exists / P.forall); the second depends on the counts of the first
+  const bool p1[6] = {decided || cd, x, (decided && decision) || vote == 1, (decided && !decision) || vote == 0,
+                      decided && decision, decided && !decision};
+  Mask<W> m1[6];
+  g.template ballots<6>(p1, m1);
+  const bool noDec = !many(m1[0]);
+  const int cntT = mpopc(m1[1]);
   const int cntF = n - cntT;
   bool ex = false;
-  if (cntF > n / 2) ex = ex || !g.any((decided && decision) || vote == 1);
-  if (cntT > n / 2) ex = ex || !g.any((decided && !decision) || vote == 0);
-  bool inv0 = noDec || ex;
-  if (c & 1) {  // after R0: P.forall(p => p.vote.isDefined ==> |{i : i.x == p.vote.get}| > n/2)
-    const bool bad = g.any((vote == 1 && !(cntT > n / 2)) || (vote == 0 && !(cntF > n / 2)));
-    inv0 = inv0 && !bad;
-  }
-  const Mask<W> D = g.ballot(decided);
-  const bool same = !(g.any(decided && decision) && g.any(decided && !decision));
-  const bool irrev = !has_old || !g.any(old_decided && !(decided && old_decision == decision));
+  if (cntF > n / 2) ex = ex || !many(m1[2]);
+  if (cntT > n / 2) ex = ex || !many(m1[3]);
+  // after R0 (c odd): P.forall(p => p.vote.isDefined ==> |{i : i.x == p.vote.get}| > n/2)
+  const bool p2[3] = {decided, (c & 1) != 0 && ((vote == 1 && !(cntT > n / 2)) || (vote == 0 && !(cntF > n / 2))),
+                      has_old && old_decided && !(decided && old_decision == decision)};
+  Mask<W> m2[3];
+  g.template ballots<3>(p2, m2);
+  const bool inv0 = (noDec || ex) && !many(m2[1]);
+  const Mask<W> D = m2[0];
+  const bool same = !(many(m1[4]) && many(m1[5]));
+  const bool irrev = !many(m2[2]);
   const uint32_t fb = fbit(inv0, 0) |
                       fbit(inv0, 1) |
                       fbit(same, 2) |
@@ -93,10 +100,15 @@ PSG_DEV void benor_body(const KArgs& a) {
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const int size = mpopc(M);
         if (!halted) hs = size;
-        pred = !g.any(!halted && size <= n / 2);
-        if ((k & 1) == 0) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
-          const Mask<W> Tm = mand(g.ballot(x), act);
-          const Mask<W> CDm = mand(g.ballot(cd), act);
+        // the round's pre-state ballots and the SafetyPredicate witness share one exchange
+        const bool even = (k & 1) == 0;
+        const bool pr[3] = {!halted && size <= n / 2, even ? x : vote == 1, even ? cd : vote == 0};
+        Mask<W> pm[3];
+        g.template ballots<3>(pr, pm);
+        pred = !many(pm[0]);
+        if (even) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
+          const Mask<W> Tm = mand(pm[1], act);
+          const Mask<W> CDm = mand(pm[2], act);
           if (!halted) {
             if (cd) {
               dec_val = x ? 1 : 0;
@@ -117,8 +129,8 @@ PSG_DEV void benor_body(const KArgs& a) {
             }
           }
         } else {  // R1: broadcast vote — BenOr.scala:57-79
-          const Mask<W> VT = mand(g.ballot(vote == 1), act);
-          const Mask<W> VF = mand(g.ballot(vote == 0), act);
+          const Mask<W> VT = mand(pm[1], act);
+          const Mask<W> VF = mand(pm[2], act);
           if (!halted) {
             const int t = mpopc(mand(M, VT));
             const int f = mpopc(mand(M, VF));
