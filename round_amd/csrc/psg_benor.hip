@@ -63,6 +63,8 @@ PSG_DEV void benor_body(const KArgs& a) {
   const int thr = a.variant == 1 ? n / 4 : n / 2;  // BenOr.scala:68, 71 (variant 1: mutation)
   const Mask<W> full = mfull<W>(n);
 
+  PhaseTimers pt;  // profiling builds only: t0 setup, t1 HO sets, t2 update, t3 finish, t4 check, t5 frozen round
+  pt.start();
   InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
   for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
@@ -87,6 +89,7 @@ PSG_DEV void benor_body(const KArgs& a) {
                    cd ? 1 : 0, hs);
     };
     if (tracing<SH>(a)) trace(0, n);
+    pt.mark(0);
     for (int k = 0; k < a.R; ++k) {
       const bool old_decided = decided, old_decision = decision;
       const Mask<W> act = g.ballot(!halted);
@@ -99,6 +102,7 @@ PSG_DEV void benor_body(const KArgs& a) {
         if (sc.crash_on) cs.sets(g, k, CB, CN);
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const int size = mpopc(M);
+        pt.mark(1);
         if (!halted) hs = size;
         // the round's pre-state ballots and the SafetyPredicate witness share one exchange
         const bool even = (k & 1) == 0;
@@ -150,12 +154,16 @@ PSG_DEV void benor_body(const KArgs& a) {
           }
         }
         if (halt_round == k) halted = true;
+        pt.mark(2);
       }
       if constexpr (!SH::kFused) benor_check<W>(g, ck, k + 1, true, n, full, x, cd, vote, decided, decision, old_decided, old_decision, pred);
       if (tracing<SH>(a)) trace(k + 1, hs);
+      pt.mark(many(act) ? 4 : 5);
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 5, dec_val, dec_round, halt_round, x ? 1 : 0, &bc);
+    pt.mark(3);
   }
+  pt.flush(a.counters, threadIdx.x & 63);
   __syncthreads();
   counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 5, a.R);
 }

@@ -1,6 +1,6 @@
 """Phase-timer probe (profiling build: PSG_LIB=round_amd/libpsg_timers.so PSG_PHASE_TIMERS=1).
 
-  python3 scripts/probe_phases.py [otr|lv|fm|kset]   # otr: headline launch at V=64 and V=2;
+  python3 scripts/probe_phases.py [otr|lv|fm|kset|benor]   # otr: headline launch at V=64 and V=2;
                                                     # lv: BASELINE C3 shard; fm / kset: C4 rows
 """
 import os
@@ -14,6 +14,8 @@ if which == "otr":
     runs = [(psync.OTR(), 64, 20, 10_000_000, dict(value_range=V), f"V {V}") for V in (64, 2)]
 elif which == "lv":
     runs = [(psync.LastVoting(), 64, 20, 12_500_000, {}, "C3")]
+elif which == "benor":
+    runs = [(psync.BenOr(), 128, 64, 1_000_000, {}, "C5 BenOr")]
 elif which == "fm":
     runs = [(psync.FloodMin(f), 256, f + 2, 1_000_000, {}, f"FloodMin f={f}") for f in (0, 8)]
 else:
