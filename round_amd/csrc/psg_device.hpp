@@ -1263,11 +1263,14 @@ PSG_DEV int32_t maxby_ts_x(Grp<W>& g, const int32_t* xs, const Mask<W>& Mc, int 
 
 template <int W>
 PSG_DEV void kagree_check(Grp<W>& g, Checks& ck, int c, int kk, const Mask<W>& full, bool decided, int32_t decision,
-                          const X0Set<W>& X0, bool crashed, const int32_t* dstaged) {
-  // decided, decided by a correct process, decided a non-initial value: one exchange
-  const bool pr[3] = {decided, decided && !crashed, decided && !X0.contains(decision)};
-  Mask<W> m[3];
-  g.template ballots<3>(pr, m);
+                          const X0Set<W>& X0, bool crashed, const int32_t* dstaged, bool alive = false,
+                          Mask<W>* alive_out = nullptr) {
+  // decided, decided by a correct process, decided a non-initial value: one exchange;
+  // alive_out: the caller's next-round `act` ballot rides on the same exchange
+  const bool pr[4] = {decided, decided && !crashed, decided && !X0.contains(decision), alive};
+  Mask<W> m[4];
+  g.template ballots<4>(pr, m);
+  if (alive_out) *alive_out = m[3];
   Mask<W> Y = m[1];
   int distinct = 0;
   while (many(Y) && distinct <= kk) {

@@ -57,21 +57,28 @@ PSG_DEV void floodmin_body(const KArgs& a) {
     Checks ck;
     ck.reset();
     typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
-    auto check = [&](int c) {
-      // W > 1: the staged decisions are published by the barrier of kagree_check's
-      // first ballot exchange (read only after it); the previous check's reads are
-      // ordered before this write by the next round's `act` exchange
-      if constexpr (W > 1) L.ds[g.pid] = decision;
-      kagree_check<W>(g, ck, c, 1, full, decided, decision, X0, crashed, L.ds);
+    // The check's first ballot exchange also carries the next round's `act` (alive
+    // processes), so a round costs one exchange fewer (fused Spec modules, which
+    // skip the built-in check, ballot it at the top of the round instead).
+    // W > 1: the staged decisions are published by the barrier of that exchange
+    // (read only after it). A write after an executed round is ordered behind the
+    // previous check's reads by the round's min exchange; after a frozen round
+    // (every process halted) the decisions are unchanged and are not rewritten.
+    Mask<W> act_next = mzero<W>();
+    auto check = [&](int c, bool restage) {
+      if constexpr (W > 1) {
+        if (restage) L.ds[g.pid] = decision;
+      }
+      kagree_check<W>(g, ck, c, 1, full, decided, decision, X0, crashed, L.ds, !halted, &act_next);
     };
-    if constexpr (!SH::kFused) check(0);
+    if constexpr (!SH::kFused) check(0, true);
     auto trace = [&](int c, int32_t hs) {
       emit_state<W, SH>(sh, g, a, i, c, x, decided ? 1 : 0, decision, 0, 0, 0, 0, 0, hs);
     };
     if (tracing<SH>(a)) trace(0, n);
     pt.mark(0);
     for (int k = 0; k < a.R; ++k) {
-      const Mask<W> act = g.ballot(!halted);
+      const Mask<W> act = SH::kFused ? g.ballot(!halted) : act_next;
       int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
         Mask<W> goodS;
@@ -120,7 +127,7 @@ PSG_DEV void floodmin_body(const KArgs& a) {
         }
       }
       pt.mark(2);
-      if constexpr (!SH::kFused) check(k + 1);
+      if constexpr (!SH::kFused) check(k + 1, many(act));
       if (tracing<SH>(a)) trace(k + 1, hs);
       pt.mark(many(act) ? 4 : 5);
     }
