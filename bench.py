@@ -31,6 +31,7 @@ from round_amd import psync  # noqa: E402
 
 B_ALG_OTR = 24  # algorithmic bytes per process-round
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+CUS = 256  # MI355X compute units (8 XCDs x 32)
 
 
 def parse():
@@ -49,9 +50,16 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic_bytes(args):
-    """HBM bytes per launch of otr_kernel<1, false, false> from the newest committed PMC summary
-    (profiles/*/pmc_summary.json, scripts/summarize_profile.py) of this exact workload."""
+def lib_sha256():
+    import hashlib
+    with open(os.path.join(ROOT, "round_amd", "libpsg.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def pmc_profile(args):
+    """The newest committed PMC summary of otr_kernel<1> on this exact workload
+    (profiles/*/pmc_summary.json, scripts/summarize_profile.py): HBM bytes per launch and
+    instructions per instance-round, with whether it was taken on this very libpsg.so."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json"))):
@@ -60,15 +68,45 @@ def pmc_traffic_bytes(args):
         except (OSError, ValueError):
             continue
         w = d.get("workload", {})
-        if ("otr_kernel<1" in d.get("kernel", "") and "hbm" in d and w.get("n") == args.n
-                and w.get("rounds") == args.rounds and w.get("instances_per_gpu") == args.instances
-                and w.get("value_range") == args.V):
-            best = (d["hbm"]["traffic_bytes"], os.path.relpath(f, ROOT), d)
-    return best
+        if ("otr_kernel<1" in d.get("kernel", "") and "hbm" in d and "per_instance_round" in d
+                and w.get("n") == args.n and w.get("rounds") == args.rounds
+                and w.get("instances_per_gpu") == args.instances and w.get("value_range") == args.V):
+            best = (os.path.relpath(f, ROOT), d)
+    if best is None:
+        return None
+    try:
+        same = best[1].get("lib_sha256") == lib_sha256()
+    except OSError:
+        same = False
+    return best[0], best[1], same
+
+
+def _cpu_quota():
+    """CPUs granted by the cgroup (cpu.max), None when unlimited or unknown."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        return None
+
+
+def _time_oracle(oracle, cfg, threads, target_s):
+    cal = 100 * threads
+    t0 = time.perf_counter()
+    oracle.run(cfg, 0, cal, threads=threads)
+    dt = time.perf_counter() - t0
+    count = max(cal, int(cal * target_s / max(dt, 1e-3)))
+    t0 = time.perf_counter()
+    s, _, _ = oracle.run(cfg, 0, count, threads=threads)
+    dt = time.perf_counter() - t0
+    return s.process_rounds / dt, count, dt
 
 
 def cpu_baseline(cfg, target_s):
-    """Time the oracle (C++ restatement, test infrastructure) on the host cores."""
+    """Time the oracle (C++ restatement of the reference's rounds + Spec, test
+    infrastructure; not the JVM reference, which cannot run here) on the host: one
+    thread per core the process may run on (all of them, os.sched_getaffinity), and one
+    thread alone. SURVEY §8d / BASELINE.md §2 ask for both rates."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.build()
@@ -76,22 +114,21 @@ def cpu_baseline(cfg, target_s):
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    cal = 200 * cores
-    t0 = time.perf_counter()
-    oracle.run(cfg, 0, cal, threads=cores)
-    dt = time.perf_counter() - t0
-    count = max(cal, int(cal * target_s / max(dt, 1e-3)))
-    t0 = time.perf_counter()
-    s, _, _ = oracle.run(cfg, 0, count, threads=cores)
-    dt = time.perf_counter() - t0
+    quota = _cpu_quota()
+    v_all, n_all, t_all = _time_oracle(oracle, cfg, cores, target_s * 2 / 3)
+    v_one, n_one, t_one = _time_oracle(oracle, cfg, 1, target_s / 3)
     return {
-        "value": s.process_rounds / dt,
+        "value": v_all,
         "unit": "process-rounds/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"{count} instances of the same workload (ids 0..{count - 1}), oracle/psg_oracle.cpp, "
-                  f"{cores} threads, {dt:.1f} s",
+        "sample": f"{n_all} instances of the same workload (ids 0..{n_all - 1}), oracle/psg_oracle.cpp, "
+                  f"{cores} threads, {t_all:.1f} s",
+        "single_core": {"value": v_one, "cores": 1,
+                        "sample": f"{n_one} instances (ids 0..{n_one - 1}), 1 thread, {t_one:.1f} s"},
+        "cgroup_cpu_quota": quota,
+        "note": "port = the build's C++ restatement of the reference (oracle/), not the JVM reference "
+                "(no JVM in the image; parity with the JVM is unpinned, DESIGN §7)",
     }
 
 
@@ -150,7 +187,8 @@ def main():
         pr_per_step = s.process_rounds  # all ranks, one step
         value = pr_per_step * steps / head["dt"]
         per_launch_pr = args.instances * args.n * args.rounds  # one rank's launch
-        achieved = per_launch_pr * B_ALG_OTR / head["kernel_s"] / 1e9
+        inst_rounds = args.instances * args.rounds
+        alg_gbs = per_launch_pr * B_ALG_OTR / head["kernel_s"] / 1e9
         out = {
             "metric": "checked process-rounds/sec (node), OTR n=64 w/ invariants; % HBM peak",
             "value": value,
@@ -176,33 +214,62 @@ def main():
                 "parallelism": f"instance-sharded x{world} (RCCL all-reduce of counters)",
             },
             "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
+                # the fused kernel keeps process state on chip (real HBM traffic ~2 % of the
+                # algorithmic bytes): its binding resource is instruction issue
+                "bound": "issue",
+                "achieved": None,
+                "peak": None,
+                "unit": "G SALU instructions/s",
+                "frac": None,
                 "traffic": None,
                 "kernel": "psg::otr_kernel<1, false, false, psg::NoHook>",  # <W, OTR2, explicit schedule, check hook>
                 "kernel_ms": head["kernel_s"] * 1e3,
-                "bytes_per_process_round": B_ALG_OTR,
+                "hbm_algorithmic": {
+                    "note": "SURVEY §8d accounting: 24 B of state per process-round as if streamed each "
+                            "round; a bookkeeping rate, not a physical bound",
+                    "bytes_per_process_round": B_ALG_OTR, "achieved": alg_gbs, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": alg_gbs / HBM_PEAK_GBS},
             },
             "checks": {
                 "violations": psync.BatchResult(psync.OTR(), args.rounds, s).violations(),
                 "termination_hist": [s.term_hist[i] for i in range(args.rounds + 2)],
                 "decided_processes": s.decided_processes,
+                # counted = n*R per instance; active = rounds a process took a step in;
+                # check-only = instance-rounds after every process halted (Spec evaluated only)
+                "process_rounds_counted": s.process_rounds,
+                "process_rounds_active": s.active_process_rounds,
+                "instance_rounds_live": s.live_instance_rounds,
+                "instance_rounds_check_only": s.instances * args.rounds - s.live_instance_rounds,
             },
             "variants": variants,
         }
-        tb = pmc_traffic_bytes(args)
-        if tb is not None:
-            out["roofline"]["traffic"] = tb[0] / head["kernel_s"] / 1e9
-            out["roofline"]["traffic_bytes_per_launch"] = tb[0]
-            out["roofline"]["traffic_source"] = tb[1] + " (PMC FETCH_SIZE*2 + WRITE_SIZE per launch)"
-            # the binding resource of this fused kernel is instruction issue: report the
-            # same profile's issue utilisation and per-instance-round instruction counts beside it
-            if "issue_utilization" in tb[2]:
-                out["roofline"]["issue_utilization"] = tb[2]["issue_utilization"]
-                out["roofline"]["insts_per_instance_round"] = tb[2].get("per_instance_round")
+        prof = pmc_profile(args)
+        if prof is not None:
+            src, d, same = prof
+            rl = out["roofline"]
+            # live rate of this run: the profile's instructions per instance-round (a property of
+            # the code, taken on the same libpsg.so when profile_matches_build) x the launch's
+            # instance-rounds / this run's kernel time; peak: one instruction per CU per cycle
+            # (SALU) / per SIMD per 2 cycles (VALU, wave64 on a 32-lane SIMD) at the profile's clock
+            ipr = d["per_instance_round"]
+            clk = d.get("clock_GHz") or 2.4
+            salu = ipr["SQ_INSTS_SALU"] * inst_rounds / head["kernel_s"] / 1e9
+            valu = ipr["SQ_INSTS_VALU"] * inst_rounds / head["kernel_s"] / 1e9
+            pk_s, pk_v = CUS * clk, CUS * 4 * clk / 2
+            pipe = "SALU" if salu / pk_s >= valu / pk_v else "VALU"
+            rl.update({"pipe": pipe, "achieved": salu if pipe == "SALU" else valu,
+                       "peak": pk_s if pipe == "SALU" else pk_v, "unit": f"G {pipe} instructions/s"})
+            rl["frac"] = rl["achieved"] / rl["peak"]
+            rl["valu"] = {"achieved": valu, "peak": pk_v, "frac": valu / pk_v, "unit": "G VALU instructions/s"}
+            rl["salu"] = {"achieved": salu, "peak": pk_s, "frac": salu / pk_s, "unit": "G SALU instructions/s"}
+            rl["insts_per_instance_round"] = ipr
+            rl["profile_issue_utilization"] = d.get("issue_utilization")
+            rl["profile"] = src
+            rl["profile_matches_build"] = same
+            rl["traffic"] = d["hbm"]["traffic_bytes"] / head["kernel_s"] / 1e9
+            rl["traffic_unit"] = "GB/s"
+            rl["traffic_bytes_per_launch"] = d["hbm"]["traffic_bytes"]
+            rl["traffic_source"] = src + " (PMC FETCH_SIZE*2 + WRITE_SIZE per launch)"
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(head["cfg"], args.cpu_seconds)
         else:

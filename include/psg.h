@@ -29,10 +29,15 @@
  *
  * Conventions: every function returns 0 on success and a negative errno-style
  * code on failure (no exception, no abort crosses the ABI). The caller owns all
- * host buffers; the library owns device memory. A context is bound to one HIP
- * device and is single-threaded. One process per GPU: multi-GPU runs shard the
- * global instance-id range across processes (results are bit-identical for any
- * sharding because every random draw is keyed on the global instance id).
+ * host buffers; the library owns device memory. A context is single-threaded.
+ * It drives one HIP device (`device`) or, with `n_devices` > 0, the listed
+ * devices: each call then splits its instance range into contiguous per-device
+ * slices, runs them on one host thread per device and sums the summaries
+ * (the reference's per-instance executor pool,
+ * psync/runtime/Runtime.scala:43-57, 126-128). The other multi-GPU form is one
+ * process per GPU, each with its own context over a shard of the global
+ * instance-id range. Results are bit-identical for any split, because every
+ * random draw is keyed on the global instance id.
  */
 #ifndef PSG_H
 #define PSG_H
@@ -44,7 +49,7 @@
 extern "C" {
 #endif
 
-#define PSG_ABI_VERSION 3u
+#define PSG_ABI_VERSION 4u
 
 /* Algorithms, keyed on the reference class names. */
 enum psg_alg {
@@ -80,6 +85,7 @@ enum psg_tiebreak {
 #define PSG_MAX_ROUNDS 250
 #define PSG_MAX_CHECKS 12
 #define PSG_NEVER 0xFFu /* "never" marker in uint8 check-point fields */
+#define PSG_MAX_DEVICES 16
 
 /* Seeded adversarial HO schedule. All randomness is Philox4x32-10 keyed by
  * (seed_lo, seed_hi) with counter (inst_lo, inst_hi, round, pid | stream<<16);
@@ -108,13 +114,16 @@ typedef struct psg_config {
   int32_t param;        /* OTR/OTR2 afterDecision (Otr.scala:89, default 2); FloodMin f (FloodMin.scala:27);
                            KSet k (KSetAgreement.scala:56); KSetEarlyStopping t; others unused */
   int32_t tiebreak;     /* enum psg_tiebreak */
-  int32_t device;       /* HIP device ordinal */
+  int32_t device;       /* HIP device ordinal (n_devices == 0) */
   int32_t variant;      /* 0 = reference algorithm; 1 = test mutation */
   uint64_t batch_capacity; /* max instances per psg_run_batch call (device buffers sized for it) */
   psg_schedule sched;
   int32_t param2;       /* KSetEarlyStopping k (KSetEarlyStopping.scala:9; param = t) */
   int32_t reserved;
   double real_param;    /* EpsilonConsensus epsilon (Epsilon.scala:16; param = f) */
+  int32_t n_devices;    /* 0: the single device `device`; 1..PSG_MAX_DEVICES: run on devices[0..n_devices)
+                           (an ordinal may repeat; batch_capacity is the whole context's, split evenly) */
+  int32_t devices[PSG_MAX_DEVICES];
 } psg_config;
 
 /* Aggregate result of one batch. All fields are sums over instances (so a
@@ -122,7 +131,12 @@ typedef struct psg_config {
  * except kernel_ns. */
 typedef struct psg_summary {
   int64_t instances;
-  int64_t process_rounds;              /* checked process-rounds = n * R per instance */
+  int64_t process_rounds;              /* checked process-rounds = n * R per instance (a
+                                          halted process counts until its instance's last check) */
+  int64_t active_process_rounds;       /* of those, rounds in which the process took a step (not yet
+                                          halted at the round's start; psync/Round.scala:42-55) */
+  int64_t live_instance_rounds;        /* instance-rounds with some process still active; the other
+                                          n_rounds * instances - live ones evaluate the Spec only */
   int64_t fail_count[PSG_MAX_CHECKS];  /* instances in which check slot was false at some check point */
   int64_t decided_processes;           /* processes whose decide callback fired */
   int64_t digest;                      /* sum (mod 2^64) of per-instance digests */
@@ -224,7 +238,11 @@ typedef struct psg_spec_program {
   int32_t n_vars;            /* bound variables used, <= 16 */
   const char* module_path;   /* NULL: interpret the bytecode; else a gfx950 code object with kernels
                                 psg_spec_native_w1..w4 (the same Spec lowered to wave code by
-                                round_amd/formula.py compile_native), launched instead */
+                                round_amd/formula.py compile_native), launched instead; a fused module
+                                also holds psg_fused_a<alg>_w<W> / psg_fused_x_a<alg>_w<W> and records
+                                its algorithm in the device global `psg_spec_alg` */
+  int32_t alg;               /* 0: not bound to an algorithm; else the enum psg_alg the program was
+                                compiled for (a mismatch with the context is PSG_EINVAL) */
 } psg_spec_program;
 
 typedef struct psg_ctx psg_ctx;

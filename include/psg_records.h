@@ -36,7 +36,7 @@ extern "C" {
 #endif
 
 #define PSG_REC_MAGIC "PSGREC\r\n" /* 8 bytes, no terminator in the file */
-#define PSG_REC_VERSION 1u
+#define PSG_REC_VERSION 2u /* 2: psg_config of ABI 4 (device list) */
 #define PSG_REC_ALIGN 64u
 #define PSG_REC_MAX_SECTIONS 16
 #define PSG_REC_NAME_BYTES 24

@@ -1,0 +1,57 @@
+/*
+ * jni_min/jni.h — a declaration-only subset of the JNI C interface (JDK jni.h) for
+ * compile-checking integration/jni/psg_jni.c in a container without a JDK
+ * (tests/test_jni_shim.py: gcc -fsyntax-only and -c against this header). It
+ * declares only the types and the JNIEnv functions the shim calls, with the JNI
+ * specification's C signatures; the function table layout is NOT the JDK's, so
+ * this header must never be used to build a library that a JVM loads.
+ */
+#ifndef PSG_JNI_MIN_H
+#define PSG_JNI_MIN_H
+
+#include <stdint.h>
+
+#define JNIEXPORT __attribute__((visibility("default")))
+#define JNICALL
+#define JNI_ABORT 2
+
+typedef int32_t jint;
+typedef int64_t jlong;
+typedef int8_t jbyte;
+typedef uint8_t jboolean;
+typedef double jdouble;
+typedef jint jsize;
+
+struct _jobject;
+typedef struct _jobject* jobject;
+typedef jobject jclass;
+typedef jobject jstring;
+typedef jobject jthrowable;
+typedef jobject jarray;
+typedef jarray jintArray;
+typedef jarray jlongArray;
+typedef jarray jbyteArray;
+typedef jarray jdoubleArray;
+
+struct JNINativeInterface_;
+typedef const struct JNINativeInterface_* JNIEnv;
+
+struct JNINativeInterface_ {
+  jclass (*FindClass)(JNIEnv* env, const char* name);
+  jint (*ThrowNew)(JNIEnv* env, jclass clazz, const char* msg);
+  jsize (*GetArrayLength)(JNIEnv* env, jarray array);
+  jlongArray (*NewLongArray)(JNIEnv* env, jsize len);
+  jint* (*GetIntArrayElements)(JNIEnv* env, jintArray array, jboolean* isCopy);
+  jlong* (*GetLongArrayElements)(JNIEnv* env, jlongArray array, jboolean* isCopy);
+  jdouble* (*GetDoubleArrayElements)(JNIEnv* env, jdoubleArray array, jboolean* isCopy);
+  void (*ReleaseIntArrayElements)(JNIEnv* env, jintArray array, jint* elems, jint mode);
+  void (*ReleaseLongArrayElements)(JNIEnv* env, jlongArray array, jlong* elems, jint mode);
+  void (*ReleaseDoubleArrayElements)(JNIEnv* env, jdoubleArray array, jdouble* elems, jint mode);
+  void (*GetIntArrayRegion)(JNIEnv* env, jintArray array, jsize start, jsize len, jint* buf);
+  void (*SetByteArrayRegion)(JNIEnv* env, jbyteArray array, jsize start, jsize len, const jbyte* buf);
+  void (*SetLongArrayRegion)(JNIEnv* env, jlongArray array, jsize start, jsize len, const jlong* buf);
+  const char* (*GetStringUTFChars)(JNIEnv* env, jstring str, jboolean* isCopy);
+  void (*ReleaseStringUTFChars)(JNIEnv* env, jstring str, const char* chars);
+};
+
+#endif /* PSG_JNI_MIN_H */

@@ -502,7 +502,7 @@ static SpecDef lv_spec() {
   return s;
 }
 
-/* example/BenOr.scala:270-295 (V = Domain[Boolean]) */
+/* example/BenOr.scala:90-115 (V = Domain[Boolean]) */
 static SpecDef benor_spec() {
   SpecDef s;
   Fm i = bv(0), j = bv(1), v = bv(2), ia = bv(3), p = bv(4);
@@ -523,7 +523,7 @@ static SpecDef benor_spec() {
       forallP(0, imp(fld(F_DECIDED, i, T_OLD),
                      and_(fld(F_DECIDED, i), eq(fld(F_DECISION, i, T_OLD), fld(F_DECISION, i)))))});
   s.termination = forallP(0, fld(F_DECIDED, i));
-  /* safetyPredicate: P.forall(p => p.HO.size > n/2), BenOr.scala:272. HO(p) is
+  /* safetyPredicate: P.forall(p => p.HO.size > n/2), BenOr.scala:92. HO(p) is
    * the effective heard-of set of the round just executed (a halted sender
    * sends nothing); a halted receiver takes no step and is vacuous. */
   s.safetyPredicate = forallP(4, gt(fld(F_HOSIZE, p), half));
@@ -792,7 +792,7 @@ struct KSet {
     return m;
   }
   bool update(P& s, int, int r, const std::vector<Msg<Payload>>& mb, Callback& cb, const Schedule&, int) {
-    if (s.decider) { /* KSetAgreement.scala:119-121 */
+    if (s.decider) { /* KSetAgreement.scala:48-50 */
       cb.decide(pick(s.t), r);
       s.decided = true; s.decision = pick(s.t);
       return true;
@@ -1250,7 +1250,7 @@ struct Direct {
       ck = {inv0 || inv1 || inv2, inv0, inv1, inv2, same, validity(), !any || (same && d0in), irrevocability()};
     } else {
       /* TrivialSpec algorithms: build-defined k-agreement + validity
-       * (KSetAgreement.scala:144). FloodMin / KSet / KSetEarlyStopping (crash-stop
+       * (KSetAgreement.scala:73). FloodMin / KSet / KSetEarlyStopping (crash-stop
        * algorithms): over never-crashed deciders; ShortLastVoting (HO model,
        * consensus): uniform, over every decider. */
       int k = alg == PSG_ALG_KSET ? kparam : alg == PSG_ALG_KSET_ES ? kparam2 : 1;
@@ -1703,6 +1703,15 @@ static int run_impl(const psg_config* cfg, uint64_t inst_begin, uint64_t count, 
       if (o.mismatch) { bad = 1; errs[t] = o.msg; }
       s.instances += 1;
       s.process_rounds += (int64_t)n * R;
+      {  // rounds each process took a step in (Round.scala:42-55: halted after its exit round)
+        int32_t live = 0;
+        for (int p = 0; p < n; ++p) {
+          const int32_t st = o.rec[p].halt_round >= 0 ? o.rec[p].halt_round + 1 : R;
+          s.active_process_rounds += st;
+          live = std::max(live, st);
+        }
+        s.live_instance_rounds += live;
+      }
       for (int c = 0; c < nck; ++c) if (o.sum.first_fail[c] != PSG_NEVER) s.fail_count[c] += 1;
       s.decided_processes += o.sum.n_decided;
       s.digest = (int64_t)((uint64_t)s.digest + o.sum.digest);
@@ -1722,6 +1731,8 @@ static int run_impl(const psg_config* cfg, uint64_t inst_begin, uint64_t count, 
   for (auto& s : part) {
     total.instances += s.instances;
     total.process_rounds += s.process_rounds;
+    total.active_process_rounds += s.active_process_rounds;
+    total.live_instance_rounds += s.live_instance_rounds;
     for (int c = 0; c < PSG_MAX_CHECKS; ++c) total.fail_count[c] += s.fail_count[c];
     total.decided_processes += s.decided_processes;
     total.digest = (int64_t)((uint64_t)total.digest + (uint64_t)s.digest);

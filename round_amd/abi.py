@@ -5,7 +5,7 @@ binding (oracle/oracle.py): both libraries speak the same C structs.
 """
 import ctypes as C
 
-PSG_ABI_VERSION = 3
+PSG_ABI_VERSION = 4
 
 PSG_ALG_OTR = 1
 PSG_ALG_LAST_VOTING = 2
@@ -31,6 +31,7 @@ PSG_MAX_N = 256
 PSG_MAX_ROUNDS = 250
 PSG_MAX_CHECKS = 12
 PSG_NEVER = 0xFF
+PSG_MAX_DEVICES = 16
 
 # Reference class name -> alg id ("Algorithm ids are keyed on the
 # reference class name").
@@ -107,6 +108,8 @@ class Config(C.Structure):
         ("param2", C.c_int32),
         ("reserved", C.c_int32),
         ("real_param", C.c_double),
+        ("n_devices", C.c_int32),
+        ("devices", C.c_int32 * PSG_MAX_DEVICES),
     ]
 
 
@@ -114,6 +117,8 @@ class Summary(C.Structure):
     _fields_ = [
         ("instances", C.c_int64),
         ("process_rounds", C.c_int64),
+        ("active_process_rounds", C.c_int64),
+        ("live_instance_rounds", C.c_int64),
         ("fail_count", C.c_int64 * PSG_MAX_CHECKS),
         ("decided_processes", C.c_int64),
         ("digest", C.c_int64),
@@ -145,12 +150,12 @@ assert C.sizeof(InstanceSummary) == 24
 assert C.sizeof(ProcessRecord) == 16
 
 # Fields of Summary that are summed across ranks (everything but kernel_ns).
-SUMMARY_SUM_FIELDS = 2 + PSG_MAX_CHECKS + 2 + (PSG_MAX_ROUNDS + 2)
+SUMMARY_SUM_FIELDS = 4 + PSG_MAX_CHECKS + 2 + (PSG_MAX_ROUNDS + 2)
 
 
 def summary_to_list(s):
     """Summary -> flat list of int64 in struct order (kernel_ns last)."""
-    out = [s.instances, s.process_rounds]
+    out = [s.instances, s.process_rounds, s.active_process_rounds, s.live_instance_rounds]
     out += list(s.fail_count)
     out += [s.decided_processes, s.digest]
     out += list(s.term_hist)
@@ -163,6 +168,8 @@ def summary_from_list(vals):
     it = iter(vals)
     s.instances = next(it)
     s.process_rounds = next(it)
+    s.active_process_rounds = next(it)
+    s.live_instance_rounds = next(it)
     for i in range(PSG_MAX_CHECKS):
         s.fail_count[i] = next(it)
     s.decided_processes = next(it)
@@ -180,6 +187,8 @@ def summary_dict(s, alg, rounds):
     return {
         "instances": s.instances,
         "process_rounds": s.process_rounds,
+        "active_process_rounds": s.active_process_rounds,
+        "live_instance_rounds": s.live_instance_rounds,
         "fail_count": {names[i]: s.fail_count[i] for i in range(len(names))},
         "decided_processes": s.decided_processes,
         "digest": s.digest & ((1 << 64) - 1),
@@ -199,6 +208,7 @@ class SpecProgram(C.Structure):
         ("term_entry", C.c_int32),
         ("n_vars", C.c_int32),
         ("module_path", C.c_char_p),
+        ("alg", C.c_int32),
     ]
 
 

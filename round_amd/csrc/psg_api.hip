@@ -12,6 +12,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/psg.h"
@@ -66,7 +67,9 @@ struct psg_ctx {
   hipModule_t module = nullptr;
   hipFunction_t native_fn = nullptr;
   hipFunction_t fused_fn = nullptr, fused_x_fn = nullptr;  // fused Spec module: round kernel + Spec
+  int32_t module_alg = 0;        // the module's psg_spec_alg (0: not recorded)
   bool staged = false;
+  bool staged_host = false;      // the staged rows came from the host (else seeded values)
   uint64_t staged_begin = 0, staged_count = 0;
   // explicit schedule (psg_load_schedule)
   uint64_t* d_ho = nullptr;
@@ -90,6 +93,9 @@ struct psg_ctx {
   uint64_t last_count = 0;
   int grid_max = 0;  // resident blocks for the algorithm's kernel
   std::string err;
+  // multi-device context (cfg.n_devices > 0): one single-device context per listed
+  // device; every call splits its range into contiguous slices, one per device
+  std::vector<psg_ctx*> subs;
 };
 
 static thread_local std::string g_create_err;
@@ -251,6 +257,8 @@ static int run_kernel(psg_ctx* c, KArgs& a, uint64_t count, psg_summary* out, bo
     std::memset(out, 0, sizeof(*out));
     out->instances = (int64_t)count;
     out->process_rounds = (int64_t)count * c->cfg.n * c->cfg.rounds;
+    out->active_process_rounds = (int64_t)host[C_ACTIVE];
+    out->live_instance_rounds = (int64_t)host[C_LIVE];
     for (int i = 0; i < PSG_MAX_CHECKS; ++i) out->fail_count[i] = (int64_t)host[C_FAIL + i];
     out->decided_processes = (int64_t)host[C_DECIDED];
     out->digest = (int64_t)host[C_DIGEST];
@@ -424,6 +432,78 @@ static int validate(const psg_config* cfg, std::string& m) {
   if (cfg->tiebreak != PSG_TIE_CHAMP && cfg->tiebreak != PSG_TIE_MIN_PID) { m = "bad tiebreak"; return PSG_EINVAL; }
   if (cfg->sched.drop_log2 > 16) { m = "drop_log2 > 16"; return PSG_EINVAL; }
   if (cfg->batch_capacity < 1) { m = "batch_capacity must be >= 1"; return PSG_EINVAL; }
+  if (cfg->n_devices < 0 || cfg->n_devices > PSG_MAX_DEVICES) { m = "n_devices out of range 0..16"; return PSG_EINVAL; }
+  return PSG_OK;
+}
+
+// ---------------------------------------------------------------- multi-device contexts
+// psg_config.n_devices > 0: the context owns one single-device context per listed
+// device. A call over instances [begin, begin+count) gives device d the contiguous
+// slice [begin + count*d/nd, begin + count*(d+1)/nd); the devices run concurrently,
+// one host thread each, and their summaries are summed (kernel_ns: the maximum).
+// Results equal a single-device run bit for bit (every draw is keyed on the global
+// instance id). Under a loaded explicit schedule a multi-device run covers exactly
+// the loaded range (its slices are the schedule's slices).
+extern "C++" {
+static void split(uint64_t count, size_t nd, size_t d, uint64_t& off, uint64_t& m) {
+  off = count * d / nd;
+  m = count * (d + 1) / nd - off;
+}
+
+template <class F>
+static int par_subs(psg_ctx* c, F&& f) {
+  const size_t nd = c->subs.size();
+  std::vector<int> rc(nd, PSG_OK);
+  std::vector<std::thread> th;
+  try {
+    th.reserve(nd);
+    for (size_t d = 1; d < nd; ++d) th.emplace_back([&rc, &f, d] { rc[d] = f(d); });
+  } catch (...) {
+    for (auto& t : th) t.join();
+    return fail(c, PSG_EIO, "could not start a host thread per device");
+  }
+  rc[0] = f(0);
+  for (auto& t : th) t.join();
+  for (size_t d = 0; d < nd; ++d)
+    if (rc[d]) return fail(c, rc[d], "device " + std::to_string(c->cfg.devices[d]) + ": " + c->subs[d]->err);
+  return PSG_OK;
+}
+
+static void summary_add(psg_summary& acc, const psg_summary& p) {
+  acc.instances += p.instances;
+  acc.process_rounds += p.process_rounds;
+  acc.active_process_rounds += p.active_process_rounds;
+  acc.live_instance_rounds += p.live_instance_rounds;
+  for (int i = 0; i < PSG_MAX_CHECKS; ++i) acc.fail_count[i] += p.fail_count[i];
+  acc.decided_processes += p.decided_processes;
+  acc.digest = (int64_t)((uint64_t)acc.digest + (uint64_t)p.digest);
+  for (int i = 0; i < PSG_MAX_ROUNDS + 2; ++i) acc.term_hist[i] += p.term_hist[i];
+  acc.kernel_ns = std::max(acc.kernel_ns, p.kernel_ns);
+}
+}  // extern "C++"
+
+static int create_multi(psg_ctx** out, const psg_config* cfg) {
+  psg_ctx* c = new (std::nothrow) psg_ctx();
+  if (!c) return PSG_ENOMEM;
+  c->cfg = *cfg;
+  c->W = (cfg->n + 63) / 64;
+  c->cap = cfg->batch_capacity;
+  const int nd = cfg->n_devices;
+  for (int d = 0; d < nd; ++d) {
+    psg_config sc = *cfg;
+    sc.n_devices = 0;
+    sc.device = cfg->devices[d];
+    sc.batch_capacity = (cfg->batch_capacity + nd - 1) / nd;
+    psg_ctx* sub = nullptr;
+    const int rc = psg_create(&sub, &sc);
+    if (rc) {
+      g_create_err = "device " + std::to_string(cfg->devices[d]) + ": " + g_create_err;
+      psg_destroy(c);
+      return rc;
+    }
+    c->subs.push_back(sub);
+  }
+  *out = c;
   return PSG_OK;
 }
 
@@ -433,6 +513,7 @@ int psg_create(psg_ctx** out, const psg_config* cfg) {
   std::string m;
   int rc = validate(cfg, m);
   if (rc) { g_create_err = m; return rc; }
+  if (cfg->n_devices > 0) return create_multi(out, cfg);
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev <= 0) { g_create_err = "no HIP device"; return PSG_ENODEV; }
@@ -476,8 +557,32 @@ int psg_create(psg_ctx** out, const psg_config* cfg) {
   return PSG_OK;
 }
 
+// multi-device psg_load_inputs / _f64: each device stages its slice
+static int multi_load_inputs(psg_ctx* c, uint64_t inst_begin, uint64_t count, const int32_t* host_init,
+                             const double* host_f64, bool f64) {
+  if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  const uint64_t n = (uint64_t)c->cfg.n, nd = c->subs.size();
+  const int rc = par_subs(c, [&](size_t d) {
+    uint64_t off, m;
+    split(count, nd, d, off, m);
+    return f64 ? psg_load_inputs_f64(c->subs[d], inst_begin + off, m, host_f64 ? host_f64 + off * n : nullptr)
+               : psg_load_inputs(c->subs[d], inst_begin + off, m, host_init ? host_init + off * n : nullptr);
+  });
+  if (rc) return rc;
+  c->staged = true;
+  c->staged_host = f64 ? host_f64 != nullptr : host_init != nullptr;
+  c->staged_begin = inst_begin;
+  c->staged_count = count;
+  return PSG_OK;
+}
+
 int psg_load_inputs(psg_ctx* c, uint64_t inst_begin, uint64_t count, const int32_t* host_init) {
   if (!c) return PSG_EINVAL;
+  if (!c->subs.empty()) {
+    if (c->cfg.alg == PSG_ALG_EPSILON && host_init)
+      return fail(c, PSG_EINVAL, "EpsilonConsensus takes Double inputs: use psg_load_inputs_f64");
+    return multi_load_inputs(c, inst_begin, count, host_init, nullptr, c->cfg.alg == PSG_ALG_EPSILON);
+  }
   if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
   if (c->cfg.alg == PSG_ALG_EPSILON) {
     if (host_init) return fail(c, PSG_EINVAL, "EpsilonConsensus takes Double inputs: use psg_load_inputs_f64");
@@ -493,6 +598,7 @@ int psg_load_inputs(psg_ctx* c, uint64_t inst_begin, uint64_t count, const int32
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->staged = true;
+  c->staged_host = host_init != nullptr;
   c->staged_begin = inst_begin;
   c->staged_count = count;
   return PSG_OK;
@@ -501,6 +607,7 @@ int psg_load_inputs(psg_ctx* c, uint64_t inst_begin, uint64_t count, const int32
 int psg_load_inputs_f64(psg_ctx* c, uint64_t inst_begin, uint64_t count, const double* host_init) {
   if (!c) return PSG_EINVAL;
   if (c->cfg.alg != PSG_ALG_EPSILON) return fail(c, PSG_EINVAL, "Double inputs are for EpsilonConsensus only");
+  if (!c->subs.empty()) return multi_load_inputs(c, inst_begin, count, nullptr, host_init, true);
   if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (host_init) {
@@ -510,13 +617,43 @@ int psg_load_inputs_f64(psg_ctx* c, uint64_t inst_begin, uint64_t count, const d
   }
   c->init_f64_host = host_init != nullptr;
   c->staged = true;
+  c->staged_host = host_init != nullptr;
   c->staged_begin = inst_begin;
   c->staged_count = count;
   return PSG_OK;
 }
 
+// multi-device psg_run_batch / psg_run_batch_spec (prog != nullptr)
+static int multi_run(psg_ctx* c, uint64_t inst_begin, uint64_t count, const psg_spec_program* prog, psg_summary* out,
+                     psg_instance_summary* per_inst) {
+  if (out) std::memset(out, 0, sizeof(*out));
+  if (count == 0) return PSG_OK;
+  if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  if (c->ho_loaded && (inst_begin != c->ho_begin || count != c->ho_count))
+    return fail(c, PSG_ERANGE, "a multi-device run under an explicit schedule covers exactly the loaded range");
+  if (!(c->staged && c->staged_begin == inst_begin && c->staged_count == count)) {
+    const int rc = psg_load_inputs(c, inst_begin, count, nullptr);  // seeded, like a single device
+    if (rc) return rc;
+  }
+  const size_t nd = c->subs.size();
+  std::vector<psg_summary> parts(nd);
+  const int rc = par_subs(c, [&](size_t d) {
+    uint64_t off, m;
+    split(count, nd, d, off, m);
+    psg_instance_summary* pi = per_inst ? per_inst + off : nullptr;
+    return prog ? psg_run_batch_spec(c->subs[d], inst_begin + off, m, prog, &parts[d], pi)
+                : psg_run_batch(c->subs[d], inst_begin + off, m, &parts[d], pi);
+  });
+  if (rc) return rc;
+  if (out)
+    for (size_t d = 0; d < nd; ++d) summary_add(*out, parts[d]);
+  c->last_count = count;
+  return PSG_OK;
+}
+
 int psg_run_batch(psg_ctx* c, uint64_t inst_begin, uint64_t count, psg_summary* out, psg_instance_summary* per_inst) {
   if (!c) return PSG_EINVAL;
+  if (!c->subs.empty()) return multi_run(c, inst_begin, count, nullptr, out, per_inst);
   if (count == 0) {
     if (out) std::memset(out, 0, sizeof(*out));
     return PSG_OK;
@@ -612,6 +749,17 @@ static uint32_t prog_fields(const psg_spec_program* p) {
 
 int psg_copy_decisions(psg_ctx* c, int32_t* decision, int32_t* decision_round) {
   if (!c) return PSG_EINVAL;
+  if (!c->subs.empty()) {  // the last batch's slices, in device order
+    const uint64_t n = (uint64_t)c->cfg.n, nd = c->subs.size();
+    for (size_t d = 0; d < nd; ++d) {
+      uint64_t off, m;
+      split(c->last_count, nd, d, off, m);
+      const int rc = psg_copy_decisions(c->subs[d], decision ? decision + off * n : nullptr,
+                                        decision_round ? decision_round + off * n : nullptr);
+      if (rc) return fail(c, rc, "device " + std::to_string(c->cfg.devices[d]) + ": " + c->subs[d]->err);
+    }
+    return PSG_OK;
+  }
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const uint64_t cells = c->last_count * (uint64_t)c->cfg.n;
   if (decision) HIPCHK(c, hipMemcpy(decision, c->d_dec, sizeof(int32_t) * cells, hipMemcpyDeviceToHost));
@@ -632,6 +780,10 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
   if (c->cfg.alg == PSG_ALG_EPSILON) return fail(c, PSG_EINVAL, "Spec programs need integer state (not EpsilonConsensus)");
   std::string m;
   if (validate_prog(prog, m)) return fail(c, PSG_EINVAL, m);
+  if (prog->alg != 0 && prog->alg != c->cfg.alg)
+    return fail(c, PSG_EINVAL, "spec program was compiled for algorithm " + std::to_string(prog->alg) +
+                                   ", the context runs " + std::to_string(c->cfg.alg));
+  if (!c->subs.empty()) return multi_run(c, inst_begin, count, prog, out, per_inst);
   if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
   if (int rc = check_sched_range(c, inst_begin, count)) return rc;
   if (out) std::memset(out, 0, sizeof(*out));
@@ -663,13 +815,24 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
     HIPCHK(c, hipModuleLoad(&c->module, prog->module_path));
     const std::string name = "psg_spec_native_w" + std::to_string(c->W);
     HIPCHK(c, hipModuleGetFunction(&c->native_fn, c->module, name.c_str()));
+    // the algorithm the module was generated for (round_amd/formula.py writes psg_spec_alg)
+    c->module_alg = 0;
+    hipDeviceptr_t gp = nullptr;
+    size_t gsz = 0;
+    if (hipModuleGetGlobal(&gp, &gsz, c->module, "psg_spec_alg") == hipSuccess && gsz == sizeof(int32_t))
+      HIPCHK(c, hipMemcpyDtoH(&c->module_alg, gp, sizeof(int32_t)));
+    (void)hipGetLastError();
     // fused modules (compile_native(fused=True)) also hold the round kernel with the Spec as its hook
-    const std::string fw = "psg_fused_w" + std::to_string(c->W), fx = "psg_fused_x_w" + std::to_string(c->W);
+    const std::string aw = "a" + std::to_string(c->cfg.alg) + "_w" + std::to_string(c->W);
+    const std::string fw = "psg_fused_" + aw, fx = "psg_fused_x_" + aw;
     if (hipModuleGetFunction(&c->fused_fn, c->module, fw.c_str()) != hipSuccess) c->fused_fn = nullptr;
     if (hipModuleGetFunction(&c->fused_x_fn, c->module, fx.c_str()) != hipSuccess) c->fused_x_fn = nullptr;
     (void)hipGetLastError();
     c->module_path = prog->module_path;
   }
+  if (native && c->module_alg != 0 && c->module_alg != c->cfg.alg)
+    return fail(c, PSG_EINVAL, "spec module " + c->module_path + " was generated for algorithm " +
+                                   std::to_string(c->module_alg) + ", the context runs " + std::to_string(c->cfg.alg));
   if (native && (c->ho_loaded ? c->fused_x_fn : c->fused_fn)) {
     // one launch: rounds + Spec from registers (no trace, no chunks)
     hipFunction_t fn = c->ho_loaded ? c->fused_x_fn : c->fused_fn;
@@ -704,6 +867,8 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
     if (out) {
       out->instances = (int64_t)count;
       out->process_rounds = (int64_t)count * c->cfg.n * c->cfg.rounds;
+      out->active_process_rounds = (int64_t)host[C_ACTIVE];
+      out->live_instance_rounds = (int64_t)host[C_LIVE];
       for (int i = 0; i < PSG_MAX_CHECKS; ++i) out->fail_count[i] = (int64_t)host[C_FAIL + i];
       out->decided_processes = (int64_t)host[C_DECIDED];
       out->digest = (int64_t)host[C_DIGEST];
@@ -787,6 +952,8 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
     acc.instances += part.instances;
     acc.process_rounds += part.process_rounds;
+    acc.active_process_rounds += part.active_process_rounds;
+    acc.live_instance_rounds += part.live_instance_rounds;
     acc.decided_processes += part.decided_processes;
     acc.digest = (int64_t)((uint64_t)acc.digest + (uint64_t)part.digest);
     acc.kernel_ns += part.kernel_ns + (int64_t)((double)ms * 1e6);
@@ -810,6 +977,17 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
 int psg_copy_decisions_f64(psg_ctx* c, double* decision, int32_t* decision_round) {
   if (!c) return PSG_EINVAL;
   if (c->cfg.alg != PSG_ALG_EPSILON) return fail(c, PSG_EINVAL, "Double decisions are for EpsilonConsensus only");
+  if (!c->subs.empty()) {
+    const uint64_t n = (uint64_t)c->cfg.n, nd = c->subs.size();
+    for (size_t d = 0; d < nd; ++d) {
+      uint64_t off, m;
+      split(c->last_count, nd, d, off, m);
+      const int rc = psg_copy_decisions_f64(c->subs[d], decision ? decision + off * n : nullptr,
+                                            decision_round ? decision_round + off * n : nullptr);
+      if (rc) return fail(c, rc, "device " + std::to_string(c->cfg.devices[d]) + ": " + c->subs[d]->err);
+    }
+    return PSG_OK;
+  }
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const uint64_t cells = c->last_count * (uint64_t)c->cfg.n;
   if (decision) HIPCHK(c, hipMemcpy(decision, c->d_dec_f64, sizeof(double) * cells, hipMemcpyDeviceToHost));
@@ -817,21 +995,95 @@ int psg_copy_decisions_f64(psg_ctx* c, double* decision, int32_t* decision_round
 }
 
 static int fetch_impl(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_summary* sums,
-                      psg_process_record* procs, double* fdec, double* fx);
+                      psg_process_record* procs, double* fdec, double* fx, bool force_seeded = false);
+
+// multi-device fetch: each id goes to the device holding its schedule slice (explicit
+// schedule) or its staged host-input slice; otherwise ids are dealt out in contiguous
+// chunks and re-executed from seeded inputs (what staged seeded rows hold anyway).
+static int multi_fetch(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_summary* sums,
+                       psg_process_record* procs, double* fdec, double* fx) {
+  if (k > c->cap) return fail(c, PSG_ERANGE, "fetch count exceeds batch_capacity");
+  const size_t nd = c->subs.size();
+  const uint64_t n = (uint64_t)c->cfg.n;
+  bool all_staged = c->staged && c->staged_host;
+  for (size_t j = 0; j < k && all_staged; ++j)
+    all_staged = ids[j] >= c->staged_begin && ids[j] - c->staged_begin < c->staged_count;
+  auto owner = [&](uint64_t id, uint64_t begin, uint64_t count) {  // device whose slice holds id
+    size_t d = (size_t)((id - begin) * nd / count);
+    uint64_t off, m;
+    for (;; ++d) {
+      split(count, nd, d, off, m);
+      if (id - begin < off + m || d + 1 == nd) return d;
+    }
+  };
+  std::vector<std::vector<size_t>> pos(nd);
+  for (size_t j = 0; j < k; ++j) {
+    size_t d;
+    if (c->ho_loaded) {
+      if (ids[j] < c->ho_begin || ids[j] - c->ho_begin >= c->ho_count)
+        return fail(c, PSG_ERANGE, "instances outside the loaded explicit schedule");
+      if (all_staged && (c->staged_begin != c->ho_begin || c->staged_count != c->ho_count))
+        return fail(c, PSG_EINVAL, "multi-device fetch: staged host inputs and the explicit schedule cover different ranges");
+      d = owner(ids[j], c->ho_begin, c->ho_count);
+    } else if (all_staged) {
+      d = owner(ids[j], c->staged_begin, c->staged_count);
+    } else {
+      d = j * nd / k;
+    }
+    pos[d].push_back(j);
+  }
+  return par_subs(c, [&](size_t d) {
+    psg_ctx* s = c->subs[d];
+    const std::vector<size_t>& P = pos[d];
+    const size_t chunk = (size_t)std::max<uint64_t>(1, s->cap);
+    std::vector<uint64_t> sid;
+    std::vector<psg_instance_summary> ss;
+    std::vector<psg_process_record> sp;
+    std::vector<double> sd, sx;
+    for (size_t a = 0; a < P.size(); a += chunk) {
+      const size_t m = std::min(chunk, P.size() - a);
+      sid.resize(m);
+      for (size_t t = 0; t < m; ++t) sid[t] = ids[P[a + t]];
+      ss.resize(m);
+      if (procs) sp.resize(m * n);
+      if (fdec) sd.resize(m * n);
+      if (fx) sx.resize(m * n);
+      const int rc = fetch_impl(s, sid.data(), m, ss.data(), procs ? sp.data() : nullptr, fdec ? sd.data() : nullptr,
+                                fx ? sx.data() : nullptr, !all_staged);
+      if (rc) return rc;
+      for (size_t t = 0; t < m; ++t) {
+        const size_t j = P[a + t];
+        if (sums) sums[j] = ss[t];
+        if (procs) std::memcpy(procs + j * n, sp.data() + t * n, sizeof(psg_process_record) * n);
+        if (fdec) std::memcpy(fdec + j * n, sd.data() + t * n, sizeof(double) * n);
+        if (fx) std::memcpy(fx + j * n, sx.data() + t * n, sizeof(double) * n);
+      }
+    }
+    return PSG_OK;
+  });
+}
 
 int psg_fetch_instances(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_summary* sums,
                         psg_process_record* procs) {
+  if (c && !c->subs.empty()) {
+    if (!ids && k) return PSG_EINVAL;
+    return multi_fetch(c, ids, k, sums, procs, nullptr, nullptr);
+  }
   return fetch_impl(c, ids, k, sums, procs, nullptr, nullptr);
 }
 
 int psg_fetch_instances_f64(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_summary* sums,
                             psg_process_record* procs, double* decision, double* final_x) {
   if (c && c->cfg.alg != PSG_ALG_EPSILON) return fail(c, PSG_EINVAL, "Double records are for EpsilonConsensus only");
+  if (c && !c->subs.empty()) {
+    if (!ids && k) return PSG_EINVAL;
+    return multi_fetch(c, ids, k, sums, procs, decision, final_x);
+  }
   return fetch_impl(c, ids, k, sums, procs, decision, final_x);
 }
 
 static int fetch_impl(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_summary* sums,
-                      psg_process_record* procs, double* fdec, double* fx) {
+                      psg_process_record* procs, double* fdec, double* fx, bool force_seeded) {
   if (!c || (!ids && k)) return PSG_EINVAL;
   if (k == 0) return PSG_OK;
   if (k > c->cap) return fail(c, PSG_ERANGE, "fetch count exceeds batch_capacity");
@@ -851,7 +1103,7 @@ static int fetch_impl(psg_ctx* c, const uint64_t* ids, size_t k, psg_instance_su
     }
     c->fetch_cap = k;
   }
-  bool in_staged = c->staged;
+  bool in_staged = c->staged && !force_seeded;
   for (size_t j = 0; j < k; ++j) {
     if (int rc = check_sched_range(c, ids[j], 1)) return rc;
     if (ids[j] < c->staged_begin || ids[j] - c->staged_begin >= c->staged_count) in_staged = false;
@@ -896,6 +1148,21 @@ int psg_load_schedule(psg_ctx* c, uint64_t inst_begin, uint64_t count, const uin
   if (!c) return PSG_EINVAL;
   if (!ho && count) return fail(c, PSG_EINVAL, "null schedule");
   if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  if (!c->subs.empty()) {
+    const uint64_t per = (uint64_t)c->cfg.rounds * (uint64_t)c->cfg.n * (uint64_t)c->W, nd = c->subs.size();
+    const int rc = par_subs(c, [&](size_t d) {
+      uint64_t off, m;
+      split(count, nd, d, off, m);
+      return psg_load_schedule(c->subs[d], inst_begin + off, m, ho ? ho + off * per : nullptr,
+                               crash_round ? crash_round + off * (uint64_t)c->cfg.n : nullptr);
+    });
+    if (rc) return rc;
+    c->ho_loaded = true;
+    c->ho_has_crash = crash_round != nullptr;
+    c->ho_begin = inst_begin;
+    c->ho_count = count;
+    return PSG_OK;
+  }
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const uint64_t n = (uint64_t)c->cfg.n, R = (uint64_t)c->cfg.rounds, W = (uint64_t)c->W;
   if (count > c->ho_cap) {
@@ -925,6 +1192,7 @@ int psg_load_schedule(psg_ctx* c, uint64_t inst_begin, uint64_t count, const uin
 
 int psg_clear_schedule(psg_ctx* c) {
   if (!c) return PSG_EINVAL;
+  for (psg_ctx* s : c->subs) (void)psg_clear_schedule(s);
   c->ho_loaded = false;
   c->ho_has_crash = false;
   c->ho_begin = c->ho_count = 0;
@@ -935,6 +1203,16 @@ int psg_materialize_schedule(psg_ctx* c, uint64_t inst_begin, uint64_t count, ui
   if (!c) return PSG_EINVAL;
   if (!ho && count) return fail(c, PSG_EINVAL, "null output");
   if (count == 0) return PSG_OK;
+  if (!c->subs.empty()) {
+    const uint64_t per = (uint64_t)c->cfg.rounds * (uint64_t)c->cfg.n * (uint64_t)c->W, nd = c->subs.size();
+    return par_subs(c, [&](size_t d) {
+      uint64_t off, m;
+      split(count, nd, d, off, m);
+      return m ? psg_materialize_schedule(c->subs[d], inst_begin + off, m, ho + off * per,
+                                          crash_round ? crash_round + off * (uint64_t)c->cfg.n : nullptr)
+               : PSG_OK;
+    });
+  }
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const uint64_t n = (uint64_t)c->cfg.n, R = (uint64_t)c->cfg.rounds, W = (uint64_t)c->W;
   const uint64_t per = R * n * W * sizeof(uint64_t);
@@ -1028,6 +1306,7 @@ static PopArgs pop_args(const psg_ctx* c, const psg_population_params* p, uint64
 
 int psg_population_fresh(psg_ctx* c, uint64_t inst_begin, uint64_t count, const psg_population_params* p) {
   if (!c) return PSG_EINVAL;
+  if (!c->subs.empty()) return fail(c, PSG_EINVAL, "device-resident populations need a single-device context");
   if (int rc = pop_check(c, p)) return rc;
   if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
   HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -1049,6 +1328,7 @@ int psg_population_fresh(psg_ctx* c, uint64_t inst_begin, uint64_t count, const 
 
 int psg_population_next(psg_ctx* c, const uint32_t* parent, const uint8_t* op, const psg_population_params* p) {
   if (!c) return PSG_EINVAL;
+  if (!c->subs.empty()) return fail(c, PSG_EINVAL, "device-resident populations need a single-device context");
   if (int rc = pop_check(c, p)) return rc;
   if (!(c->ho_loaded && c->staged && c->staged_begin == c->ho_begin && c->staged_count == c->ho_count) ||
       c->pop_cap < c->ho_count)
@@ -1080,6 +1360,7 @@ int psg_population_next(psg_ctx* c, const uint32_t* parent, const uint8_t* op, c
 
 int psg_population_read(psg_ctx* c, const uint32_t* rows, size_t k, uint64_t* ho, int32_t* init) {
   if (!c || (!rows && k) || (!ho && k)) return PSG_EINVAL;
+  if (!c->subs.empty()) return fail(c, PSG_EINVAL, "device-resident populations need a single-device context");
   if (!c->ho_loaded) return fail(c, PSG_EINVAL, "no population loaded");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const uint64_t n = (uint64_t)c->cfg.n, R = (uint64_t)c->cfg.rounds, W = (uint64_t)c->W;
@@ -1097,6 +1378,11 @@ const char* psg_last_error(const psg_ctx* c) { return c ? c->err.c_str() : g_cre
 
 void psg_destroy(psg_ctx* c) {
   if (!c) return;
+  if (!c->subs.empty() || c->cfg.n_devices > 0) {  // multi-device: the per-device contexts own everything
+    for (psg_ctx* s : c->subs) psg_destroy(s);
+    delete c;
+    return;
+  }
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->d_init) (void)hipFree(c->d_init);

@@ -13,7 +13,7 @@ namespace psg {
 
 // Slots: 0 Safety, 1 Invariant0 (with roundInvariants(0)(0) after R0),
 // 2 Agreement, 3 Irrevocability, 4 SafetyPredicate (|HO(p)| > n/2 on the
-// effective heard-of sets, BenOr.scala:272).
+// effective heard-of sets, BenOr.scala:92).
 template <int W>
 PSG_DEV void benor_check(Grp<W>& g, Checks& ck, int c, bool has_old, int n, const Mask<W>& full, bool x, bool cd,
                          int vote, bool decided, bool decision, bool old_decided, bool old_decision, bool pred) {

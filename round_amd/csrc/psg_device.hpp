@@ -90,7 +90,10 @@ struct PopArgs {
 #define PSG_PHASE_TIMERS 0
 #endif
 // global counter layout (uint64 each)
-enum { C_FAIL = 0, C_DECIDED = PSG_MAX_CHECKS, C_DIGEST = PSG_MAX_CHECKS + 1, C_HIST = PSG_MAX_CHECKS + 2,
+enum { C_FAIL = 0, C_DECIDED = PSG_MAX_CHECKS, C_DIGEST = PSG_MAX_CHECKS + 1,
+       C_ACTIVE = PSG_MAX_CHECKS + 2,  // process-rounds in which the process took a step
+       C_LIVE = PSG_MAX_CHECKS + 3,    // instance-rounds with some process still active
+       C_HIST = PSG_MAX_CHECKS + 4,
        NCOUNTERS = C_HIST + PSG_MAX_ROUNDS + 2,
        // profiling builds only (-DPSG_PHASE_TIMERS=1): per-phase shader cycles summed over waves
        // (4 phase slots, then wave-lifetime s_memrealtime ticks summed, ~min start, max end, waves)
@@ -548,6 +551,14 @@ struct Grp {
 #undef PSG_RED64
     return (int64_t)readlane64((uint64_t)v, 63);
   }
+  // sum of a per-lane 32-bit value over the wave (DPP inclusive scan, total in lane 63)
+  PSG_DEV static uint32_t wave_sum32(uint32_t v) {
+#define PSG_SUM32(C, R) v += (uint32_t)dpp32<C, R>(0, (int32_t)v);
+    PSG_SUM32(0x111, 0xF) PSG_SUM32(0x112, 0xF) PSG_SUM32(0x114, 0xF) PSG_SUM32(0x118, 0xF)
+    PSG_SUM32(0x142, 0xA) PSG_SUM32(0x143, 0xC)
+#undef PSG_SUM32
+    return (uint32_t)__builtin_amdgcn_readlane((int32_t)v, 63);
+  }
   PSG_DEV int64_t wave_min64(int64_t v) const { return dpp_reduce64<false>(v); }
   PSG_DEV int64_t wave_max64(int64_t v) const { return dpp_reduce64<true>(v); }
   PSG_DEV uint64_t wave_sum64(uint64_t v) const {
@@ -953,6 +964,7 @@ struct BlockCounters {
   unsigned int decided;
   unsigned int hist[PSG_MAX_ROUNDS + 2];
   unsigned long long digest;
+  unsigned long long active, live;  // C_ACTIVE / C_LIVE partial sums
 };
 
 PSG_DEV void counters_init(BlockCounters* bc) {
@@ -961,6 +973,8 @@ PSG_DEV void counters_init(BlockCounters* bc) {
   if (threadIdx.x == 0) {
     bc->decided = 0;
     bc->digest = 0;
+    bc->active = 0;
+    bc->live = 0;
   }
 }
 
@@ -972,6 +986,8 @@ PSG_DEV void counters_flush(BlockCounters* bc, unsigned long long* g, int ncheck
   if (threadIdx.x == 0) {
     atomicAdd(&g[C_DECIDED], (unsigned long long)bc->decided);
     atomicAdd(&g[C_DIGEST], bc->digest);
+    atomicAdd(&g[C_ACTIVE], bc->active);
+    atomicAdd(&g[C_LIVE], bc->live);
   }
 }
 
@@ -985,6 +1001,10 @@ PSG_DEV void finish_instance(Grp<W>& g, const KArgs& a, uint64_t i, const Checks
   const uint64_t d = g.valid ? proc_digest(g.pid, dec_val, dec_round, halt_round, main_x) : 0ull;
   const uint64_t dig = g.sum64(d);
   const int nd = mpopc(g.ballot(decided));
+  // rounds in which this process took a step: up to and including its halting round
+  const int32_t steps = g.valid ? (halt_round >= 0 ? halt_round + 1 : a.R) : 0;
+  const uint32_t wave_steps = Grp<W>::wave_sum32((uint32_t)steps);
+  const int32_t live = g.max32(steps, true);  // rounds executed for the instance
   if (g.valid) {
     const uint64_t off = i * (uint64_t)n + (uint64_t)g.pid;
     if (a.out_decision) a.out_decision[off] = dec_val;
@@ -1015,8 +1035,10 @@ PSG_DEV void finish_instance(Grp<W>& g, const KArgs& a, uint64_t i, const Checks
       atomicAdd(&bc->hist[term == PSG_NEVER ? a.R + 1 : term], 1u);
       atomicAdd(&bc->decided, (unsigned int)nd);
       atomicAdd(&bc->digest, (unsigned long long)dig);
+      atomicAdd(&bc->live, (unsigned long long)live);
     }
   }
+  if (g.lane == 0) atomicAdd(&bc->active, (unsigned long long)wave_steps);
 }
 
 // Process state at check point c for the Spec-program interpreter

@@ -219,7 +219,7 @@ PSG_DEV void kset_body(const KArgs& a) {
           tnew = load_t<W>(ts, qs);
           becomeDecider = true;
         }
-        if (!halted && isDec) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:119-121)
+        if (!halted && isDec) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:48-50)
           const int32_t v = kset_pick<W>(t, x0s, Emin, xmin);
           dec_val = v;
           dec_round = k;

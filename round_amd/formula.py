@@ -234,6 +234,27 @@ class Comprehension:
     def contains(self, e):
         return Contains(self, e)
 
+    # Scala Set operations on the comprehension, lowered to exactly the shapes
+    # FormulaExtractor gives them (tests/macros/FormulaExtractorSuite.scala:42-56):
+    #   s.forall(p) -> ForAll(v, Implies(In(v, s), p(v)))
+    #   s.exists(p) -> Exists(v, And(In(v, s), p(v)))
+    #   s.filter(p) -> Comprehension(v, And(In(v, s), p(v)))
+    #   s.count(p)  -> Cardinality(Comprehension(v, And(In(v, s), p(v))))
+    def forall(self, fn: Callable):
+        v = Var("proc")
+        return Quant("forall", v, Implies(Contains(self, v), fn(v)))
+
+    def exists(self, fn: Callable):
+        v = Var("proc")
+        return Quant("exists", v, And(Contains(self, v), fn(v)))
+
+    def filter(self, fn: Callable):
+        v = Var("proc")
+        return Comprehension(v, And(Contains(self, v), fn(v)))
+
+    def count(self, fn: Callable):
+        return self.filter(fn).size
+
 
 def lift(v):
     if isinstance(v, Expr):
@@ -345,6 +366,7 @@ class Program:
         self.code, self.slot_entry, self.slot_flags = list(code), list(slot_entry), list(slot_flags)
         self.term_entry, self.n_vars, self.slot_names, self.fields = term_entry, n_vars, list(slot_names), fields
         self.module_path = None  # native code object (compile_native) or None: bytecode interpreter
+        self.alg = 0             # enum psg_alg the program was compiled for (0: unbound)
         self._keep = None
 
     def to_c(self) -> abi.SpecProgram:
@@ -361,6 +383,7 @@ class Program:
         p.term_entry = self.term_entry
         p.n_vars = self.n_vars
         p.module_path = self.module_path.encode() if self.module_path else None
+        p.alg = int(self.alg or 0)
         return p
 
 
@@ -564,7 +587,9 @@ def compile_spec(spec: Spec, alg: Optional[int] = None) -> Program:
         raise FormulaError("a Spec needs at least one invariant, property or safety predicate")
     if len(entries) > abi.PSG_MAX_CHECKS:
         raise FormulaError(f"more than {abi.PSG_MAX_CHECKS} check slots")
-    return Program(comp.code, entries, flags, term, comp.max_slot + 1, names, comp.fields_used)
+    prog = Program(comp.code, entries, flags, term, comp.max_slot + 1, names, comp.fields_used)
+    prog.alg = int(alg or 0)
+    return prog
 
 
 # --------------------------------------------------------------------------- the reference specs, restated
@@ -1002,6 +1027,7 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
         "};",
         "}  // namespace psg",
         "PSG_SPEC_NATIVE_KERNELS(psg::GenSpec)",
+        f'extern "C" __device__ int32_t psg_spec_alg = {int(alg or 0)};  // checked by psg_run_batch_spec',
         "",
     ]
     return "\n".join(src), prog
@@ -1022,13 +1048,14 @@ FUSED_KERNELS = {
 
 def _fused_source(alg: int, waves: Sequence[int]) -> str:
     """The algorithm's round kernel instantiated with the generated Spec as its hook:
-    extern "C" psg_fused_w<W> (seeded HO sets) / psg_fused_x_w<W> (explicit)."""
+    extern "C" psg_fused_a<alg>_w<W> (seeded HO sets) / psg_fused_x_a<alg>_w<W> (explicit)."""
     src, body, targs = FUSED_KERNELS[alg]
     out = [f'#include "{src}"  // its kernel bodies; host launchers are compiled out (PSG_FUSED_MODULE)']
     for W in waves:
         threads = 256 if W == 1 else 64 * W
         for suffix, xho in (("", "false"), ("x_", "true")):
-            out.append(f'extern "C" __global__ void __launch_bounds__({threads}) psg_fused_{suffix}w{W}(psg::KArgs a) {{')
+            out.append(f'extern "C" __global__ void __launch_bounds__({threads}) '
+                       f'psg_fused_{suffix}a{alg}_w{W}(psg::KArgs a) {{')
             out.append(f"  psg::{body}<{targs.format(W=W)}, {xho}, psg::spec::SpecHook<psg::GenSpec>>(a);")
             out.append("}")
     return "\n".join(out) + "\n"

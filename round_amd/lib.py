@@ -82,7 +82,7 @@ def load():
 
 
 class Context:
-    """One psg_ctx (one HIP device)."""
+    """One psg_ctx: one HIP device, or several (cfg.n_devices, one host thread per device)."""
 
     def __init__(self, cfg: abi.Config):
         L = load()

@@ -123,7 +123,7 @@ class FloodMin(Algorithm):
 
 
 class KSetAgreement(Algorithm):
-    """example.KSetAgreement(rt, k, timeout) — example/KSetAgreement.scala:141."""
+    """example.KSetAgreement(rt, k, timeout) — example/KSetAgreement.scala:70-87."""
     class_name = "example.KSetAgreement"
     alg_id = abi.PSG_ALG_KSET
 
@@ -141,7 +141,7 @@ class KSetAgreement(Algorithm):
 
 
 class BenOr(Algorithm):
-    """example.BenOr(rt, timeout) — example/BenOr.scala:266."""
+    """example.BenOr(rt, timeout) — example/BenOr.scala:86-124."""
     class_name = "example.BenOr"
     alg_id = abi.PSG_ALG_BENOR
     phase_length = 2
@@ -226,8 +226,9 @@ ALGORITHMS = {c.class_name: c for c in (OTR, LastVoting, FloodMin, KSetAgreement
 def make_config(alg: Algorithm, n: int, rounds: Optional[int] = None, seed: int = 1,
                 schedule: Optional[HOSchedule] = None, value_range: Optional[int] = None,
                 tiebreak: int = abi.PSG_TIE_CHAMP, device: int = 0,
-                batch_capacity: int = 1 << 20) -> abi.Config:
-    """Build a psg_config (the reference's `new OTR(rt, ...)` + RTOptions)."""
+                batch_capacity: int = 1 << 20, devices: Optional[Sequence[int]] = None) -> abi.Config:
+    """Build a psg_config (the reference's `new OTR(rt, ...)` + RTOptions). `devices`:
+    run every batch split over these HIP devices (one host thread each) instead of `device`."""
     if not (1 <= n <= abi.PSG_MAX_N):
         raise ValueError(f"n={n} out of range 1..{abi.PSG_MAX_N}")
     c = abi.Config()
@@ -247,6 +248,12 @@ def make_config(alg: Algorithm, n: int, rounds: Optional[int] = None, seed: int 
     c.variant = alg.variant
     c.batch_capacity = batch_capacity
     c.sched = (schedule or alg.default_schedule(n)).to_c()
+    if devices:
+        if len(devices) > abi.PSG_MAX_DEVICES:
+            raise ValueError(f"at most {abi.PSG_MAX_DEVICES} devices per context")
+        c.n_devices = len(devices)
+        for i, d in enumerate(devices):
+            c.devices[i] = int(d)
     return c
 
 
@@ -288,10 +295,12 @@ class GpuRound:
 
     def __init__(self, alg: Algorithm, n: int, rounds: Optional[int] = None, seed: int = 1,
                  schedule: Optional[HOSchedule] = None, value_range: Optional[int] = None,
-                 tiebreak: int = abi.PSG_TIE_CHAMP, device: int = 0, batch_capacity: int = 1 << 20):
+                 tiebreak: int = abi.PSG_TIE_CHAMP, device: int = 0, batch_capacity: int = 1 << 20,
+                 devices: Optional[Sequence[int]] = None):
         from . import lib
         self.alg = alg
-        self.cfg = make_config(alg, n, rounds, seed, schedule, value_range, tiebreak, device, batch_capacity)
+        self.cfg = make_config(alg, n, rounds, seed, schedule, value_range, tiebreak, device, batch_capacity,
+                               devices)
         self._ctx = lib.Context(self.cfg)
 
     @property
@@ -314,6 +323,9 @@ class GpuRound:
         of the built-in checks. Returns (BatchResult-like summary, slot names)."""
         from . import formula
         prog = spec if isinstance(spec, formula.Program) else formula.compile_spec(spec, self.alg.alg_id)
+        if prog.alg and prog.alg != self.alg.alg_id:
+            raise ValueError(f"Spec program was compiled for algorithm {prog.alg}, this GpuRound runs "
+                             f"{self.alg.class_name} ({self.alg.alg_id})")
         s, pi = self._ctx.run_batch_spec(inst_begin, count, prog, per_instance)
         return SpecResult(prog.slot_names, self.cfg.rounds, s, pi)
 

@@ -21,7 +21,7 @@ import numpy as np
 from . import abi
 
 MAGIC = b"PSGREC\r\n"
-VERSION = 1
+VERSION = 2  # 2: psg_config of ABI 4 (device list)
 ALIGN = 64
 MAX_SECTIONS = 16
 NAME_BYTES = 24
@@ -200,6 +200,7 @@ def replay(path_or_records, device=0, compare=True):
     cfg = abi.Config()
     C.memmove(C.byref(cfg), C.byref(rec.cfg), C.sizeof(abi.Config))
     cfg.device = device
+    cfg.n_devices = 0  # replay on the one given device, whatever the recording context drove
     ids = np.asarray(rec.ids, np.uint64)
     # contiguous id ranges replay as batches; the file's rows are in id order per range
     out = np.zeros(rec.count, SUMMARY_DTYPE)

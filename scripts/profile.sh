@@ -21,6 +21,7 @@ step() {  # step <name> <timeout-s> <cmd...>
   esac
 }
 
+sha256sum "$ROOT/round_amd/libpsg.so" | cut -d' ' -f1 > "$OUT/lib_sha256.txt"
 B="python3 $ROOT/bench.py"
 SMALL="--steps 2 --warmup 1 --variants= --no-cpu-baseline"
 

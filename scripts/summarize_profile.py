@@ -89,5 +89,8 @@ if os.path.exists(bench):
             b = json.loads(line)
             json.dump(b, open(os.path.join(args.dst, "bench.json"), "w"), indent=1)
             out["workload"] = {k: b["config"].get(k) for k in ("n", "rounds", "instances_per_gpu", "value_range")}
+sha = os.path.join(args.src, "lib_sha256.txt")
+if os.path.exists(sha):  # the libpsg.so the profile ran (bench.py checks it against its own)
+    out["lib_sha256"] = open(sha).read().strip()
 json.dump(out, open(os.path.join(args.dst, "pmc_summary.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))

@@ -68,6 +68,18 @@ def witness_shapes():
     ])
 
 
+def set_operations():
+    """Set forall / exists / filter / count of a comprehension, lowered like
+    FormulaExtractorSuite.scala:42-56 (tests/test_formula_shapes.py)."""
+    S = P.filter(lambda i: i.x > 1)
+    return F.Spec(properties=[
+        ("SetForall", S.forall(lambda v: v.x > 2)),
+        ("SetExists", S.exists(lambda v: v.x <= 2)),
+        ("SetCount", S.count(lambda v: v.x <= 2) <= n // 2),
+        ("SetFilter", S.filter(lambda v: v.decided).size == P.filter(lambda v: v.decided & (v.x > 1)).size),
+    ])
+
+
 # (id, algorithm, n, make_config kwargs, spec factory)
 CUSTOM = [
     ("fm-n12", psync.FloodMin(2), 12, dict(value_range=8, schedule=H(drop_log2=0, good_round=0.0, crash_fmax=3)),
@@ -84,6 +96,9 @@ CUSTOM = [
     ("otr2-n12", psync.OTR2(), 12, dict(value_range=4), uniform_agreement),
     ("otr-n16-shapes", psync.OTR(), 16, dict(value_range=3), witness_shapes),
     ("otr2-n100-shapes", psync.OTR2(), 100, dict(value_range=3), witness_shapes),
+    ("otr-n12-sets", psync.OTR(), 12, dict(value_range=3), set_operations),
+    ("fm-n70-sets", psync.FloodMin(2), 70, dict(value_range=4, schedule=H(drop_log2=0, good_round=0.0,
+                                                                            crash_fmax=3)), set_operations),
     ("fm-n8-shapes", psync.FloodMin(2), 8, dict(value_range=3, schedule=H(drop_log2=0, good_round=0.0,
                                                                            crash_fmax=3)), witness_shapes),
 ]

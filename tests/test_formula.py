@@ -101,4 +101,5 @@ def test_fused_lowering_builds(alg):
     import os
     assert os.path.getsize(prog.module_path) > 1000
     src = open(prog.module_path[:-3] + ".hip").read()
-    assert "psg_fused_w1" in src and "psg_fused_x_w1" in src
+    assert f"psg_fused_a{alg}_w1" in src and f"psg_fused_x_a{alg}_w1" in src
+    assert f"psg_spec_alg = {alg};" in src and prog.alg == alg

@@ -72,6 +72,7 @@ CASES = [
 def _cmp_summary(g, o, rounds):
     assert g.instances == o.instances
     assert g.process_rounds == o.process_rounds
+    assert (g.active_process_rounds, g.live_instance_rounds) == (o.active_process_rounds, o.live_instance_rounds)
     assert list(g.fail_count) == list(o.fail_count)
     assert g.decided_processes == o.decided_processes
     assert g.digest == o.digest

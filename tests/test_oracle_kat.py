@@ -3,9 +3,9 @@
 The reference ships no golden vectors for this path, so the
 oracle is pinned by:
   * executions hand-traced line by line from the Scala sources
-    (example/Otr.scala:59-81, example/LastVoting.scala:239-336,
-    example/FloodMin.scala:21-31, example/KSetAgreement.scala:113-133,
-    example/BenOr.scala:210-262, example/Otr2.scala:38-61,
+    (example/Otr.scala:59-81, example/LastVoting.scala:111-208,
+    example/FloodMin.scala:21-31, example/KSetAgreement.scala:46-63,
+    example/BenOr.scala:30-82, example/Otr2.scala:38-61,
     example/ShortLastVoting.scala:34-98, example/KSetEarlyStopping.scala:29-41)
     on explicit HO schedules;
   * the reference's own mmor specification (src/test/scala/psync/logic/OtrExample.scala:67-75);

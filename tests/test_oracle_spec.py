@@ -88,7 +88,7 @@ def test_epsilon_mutant_is_caught(oracle_mod):
 
 @pytest.mark.parametrize("n", [4, 8, 16])
 def test_benor_violations_only_after_safety_predicate_breaks(n, oracle_mod):
-    """BenOr's invariant assumes |HO(p)| > n/2 (BenOr.scala:272). Deciders exit, so
+    """BenOr's invariant assumes |HO(p)| > n/2 (BenOr.scala:92). Deciders exit, so
     the effective heard-of sets shrink and the assumption can break; no
     violation may precede that."""
     cfg = psync.make_config(psync.BenOr(), n, seed=31)
