@@ -505,6 +505,17 @@ struct Grp {
     }
   }
   PSG_DEV bool any(bool pred) { return many(ballot(pred)); }
+  // ballot() without the valid-lane mask (W == 1: one compare, no scalar AND); for
+  // callers that only intersect the result with masks of valid processes
+  PSG_DEV Mask<W> ballot_any(bool pred) {
+    if constexpr (W == 1) {
+      Mask<W> m;
+      m.w[0] = __builtin_amdgcn_ballot_w64(pred);
+      return m;
+    } else {
+      return ballot(pred);
+    }
+  }
 
   // value of process q (uniform q): W==1 readlane of `mine`; W>1 from a staged LDS array.
   PSG_DEV int32_t bcast(int32_t mine, const int32_t* staged, int q) const {
@@ -1158,6 +1169,15 @@ struct X0Set {
     return !g.any(mtest(need, g.pid) && !contains(v));
   }
 
+  // 1 unless v sits in one of its two home slots: 0 proves membership, 1 means
+  // "maybe not a member" (resolve with contains / all_in). The sentinel value itself
+  // always answers 1.
+  PSG_DEV uint32_t maybe_out01(int32_t v) const {
+    const uint32_t h = slot(v);
+    const int32_t t0 = tab[h];
+    const int32_t t1 = tab[(h + 1) & (uint32_t)(kSlots - 1)];
+    return (ne01(t0, v) & ne01(t1, v)) | eq01(v, kEmpty);
+  }
   // contains() as a VALU 0/1 integer (see nz01); same probing scheme
   PSG_DEV uint32_t contains01(int32_t v) const {
     const uint32_t h = slot(v);

@@ -23,15 +23,18 @@ struct OtrLds {
 
 // Spec check at check point c (spec r = c). Slots: 0 Safety (some invariant
 // holds), 1..3 invariants, 4 Agreement, 5 Validity, 6 Integrity, 7 Irrevocability.
-// Every formula is evaluated from scratch at every check point. Each universally
-// quantified part is one ballot of its per-process witness:
+// Every formula is evaluated from scratch at every check point. The universally
+// quantified parts are per-process witnesses:
 //   !(i.x == init(j.x) for some j)                  keepInit   (X0-set probe)
-//   i.decided && i.decision != d0                   Agreement  (d0 = a decided value)
 //   i.decided && i.decision not initial             Validity
+//   i.decided && i.decision != d0                   Agreement  (d0 = a decided value)
 //   old(i.decided) && !(i.decided && old(i.decision) == i.decision)  Irrevocability
-// (Packing the witnesses into one word and OR-reducing it with a DPP pass was
-// measured 28 % slower on the headline launch: the DPP chain's latency outweighs
-// the scalar mask work it removes, profiles/s2_ab/ab5.log.)
+// Fast path: one VALU word per process holds a bit per witness, where the two X0
+// probes only look at the value's two home slots ("maybe not initial"); one ballot
+// of "some bit set" settles all four when no process is even a possible witness
+// (the common case). Otherwise each is resolved exactly with its own ballot and
+// the full probe. (OR-reducing such a word with a DPP chain was measured 28 %
+// slower, profiles/s2_ab/ab5.log: the chain's latency; a compare + ballot has none.)
 // V.exists(v => |{i : i.x == v}| > 2n/3 && all decisions == v): with decisions only
 // v = d0 can qualify; without, v must be a strict majority (Boyer-Moore candidate).
 template <int W, bool V2>
@@ -46,11 +49,17 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
   const Mask<W> D = g.ballot(dec01 != 0u);
   const bool anyD = many(D);
   const int32_t d0 = anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
-  const bool keep = V2 || X0.all_in(g, full, x);                     // keepInit (OTR only)
-  const bool validity = X0.all_in(g, D, decision);                   // decisions are initial values
-  const bool same = !many(mand(D, g.ballot(decision != d0)));        // Agreement
-  const Mask<W> OLD = g.ballot(old01 != 0u);                         // Irrevocability
-  const bool irrev = !has_old || !many(mandn(OLD, mand(D, g.ballot(old_decision == decision))));
+  uint32_t wit = X0.maybe_out01(decision) | ne01(decision, d0);
+  if constexpr (!V2) wit = (wit & dec01) | X0.maybe_out01(x);  // keepInit (OTR only)
+  else wit &= dec01;
+  if (has_old) wit |= old01 & (1u - (dec01 & eq01(old_decision, decision)));
+  bool keep = true, validity = true, same = true, irrev = true;
+  if (g.any((wit & valid01) != 0u)) {  // exact resolution, one ballot per formula
+    if constexpr (!V2) keep = X0.all_in(g, full, x);
+    validity = X0.all_in(g, D, decision);
+    same = !many(mand(D, g.ballot(decision != d0)));
+    if (has_old) irrev = !many(mandn(g.ballot(old01 != 0u), mand(D, g.ballot(old_decision == decision))));
+  }
   const int32_t ref = anyD ? d0 : majority_candidate<W>(g, x);
   const int cnt = mpopc(g.ballot((valid01 & eq01(x, ref)) != 0u));
   const bool condv = !anyD || same;
@@ -133,23 +142,28 @@ PSG_DEV void otr_body(const KArgs& a) {
         if (tracing<SH>(a)) hs = halted01 ? n : msize;
         const uint32_t upd = (1u - halted01) & gt01(msize, thr);
         if (g.any(upd != 0u)) {
+          // mmor: max multiplicity, ties -> smaller value (OtrExample.scala:67-75).
+          // The running best is one 64-bit key (count << 32 | v ^ 0x7FFFFFFF): a larger
+          // key has a larger count, or the same count and a smaller v, so one 64-bit
+          // compare keeps it. The loop walks xv = x ^ 0x7FFFFFFF (the key's low word).
+          // E needs neither `& act` nor the valid-lane mask: M lies inside act and rem
+          // only loses bits.
+          const int32_t xv = x ^ 0x7FFFFFFF;
           if constexpr (W > 1) {
-            L.xs[g.pid] = x;
+            L.xs[g.pid] = xv;
             __syncthreads();
           }
-          // mmor: max multiplicity, ties -> smaller value (OtrExample.scala:67-75)
           Mask<W> rem = act;
-          int32_t best_c = 0;
-          int32_t best_v = INT32_MAX;
+          uint64_t best = (uint64_t)(uint32_t)(INT32_MAX ^ 0x7FFFFFFF);  // count 0, v = INT32_MAX
           while (many(rem)) {
-            const int32_t v = g.bcast(x, L.xs, mfirst(rem));
-            const Mask<W> E = mand(g.ballot(x == v), act);
+            const int32_t kv = g.bcast(xv, L.xs, mfirst(rem));
+            const Mask<W> E = g.ballot_any(xv == kv);
             rem = mandn(rem, E);
-            const int32_t cnt = mpopc(mand(M, E));
-            const uint32_t better = gt01(cnt, best_c) | (eq01(cnt, best_c) & gt01(best_v, v));
-            best_c = better ? cnt : best_c;
-            best_v = better ? v : best_v;
+            const uint64_t key = ((uint64_t)(uint32_t)mpopc(mand(M, E)) << 32) | (uint32_t)kv;
+            best = key > best ? key : best;
           }
+          const int32_t best_c = (int32_t)(best >> 32);
+          const int32_t best_v = (int32_t)((uint32_t)best ^ 0x7FFFFFFFu);
           // x = mmor; decide on > 2n/3 copies, callback only the first time (Otr.scala:64-73)
           x = upd ? best_v : x;
           const uint32_t newdec = upd & gt01(best_c, thr);
