@@ -1137,13 +1137,37 @@ struct X0Set {
   static constexpr int32_t kEmpty = INT32_MIN;
   int32_t* tab;
   bool has_empty;  // the sentinel value itself is an initial value
+  // W == 1 with every initial value in [lo, lo + 64): the set is the 64-bit word bm
+  // (bit v - lo), kept in registers, and membership is one shift and mask: no hash,
+  // no LDS round trip (OTR / LastVoting synthetic values span {1..V}, V <= 64)
+  bool bmode;
+  int32_t lo;
+  uint64_t bm;
 
   PSG_DEV static uint32_t slot(int32_t v) {
     constexpr int kBits = W == 1 ? 7 : (W == 2 ? 8 : 9);  // log2(kSlots)
     return ((uint32_t)v * 0x9E3779B1u) >> (32 - kBits);
   }
+  PSG_DEV uint32_t bm_in01(int32_t v) const {
+    const uint32_t d = (uint32_t)v - (uint32_t)lo;  // < 64 exactly when v - lo is in [0, 64)
+    return d < 64u ? (uint32_t)(bm >> d) & 1u : 0u;
+  }
   PSG_DEV void build(Grp<W>& g, int32_t* lds, int32_t x0) {
     tab = lds;
+    bmode = false;
+    lo = 0;
+    bm = 0;
+    if constexpr (W == 1) {
+      const int32_t mn = g.min32(x0, true), mx = g.max32(x0, true);
+      if ((int64_t)mx - (int64_t)mn < 64) {
+        bmode = true;
+        lo = mn;
+        const uint64_t bit = g.valid ? 1ull << ((uint32_t)(x0 - mn) & 63u) : 0ull;
+        bm = (uint64_t)wave_or((uint32_t)bit) | ((uint64_t)wave_or((uint32_t)(bit >> 32)) << 32);
+        has_empty = false;
+        return;
+      }
+    }
     for (int t = g.pid; t < kSlots; t += 64 * W) tab[t] = kEmpty;
     lds_sync<W>();
     if (g.valid && x0 != kEmpty) {
@@ -1161,6 +1185,7 @@ struct X0Set {
   // Fast path: one ballot of "v is in neither of its two home slots"; the probe
   // loop runs only for lanes that miss both (load <= 1/2 makes that rare).
   PSG_DEV bool all_in(Grp<W>& g, const Mask<W>& sel, int32_t v) const {
+    if (bmode) return !many(mand(g.ballot(bm_in01(v) == 0u), sel));
     const uint32_t h = slot(v);
     const int32_t t0 = tab[h];
     const int32_t t1 = tab[(h + 1) & (uint32_t)(kSlots - 1)];
@@ -1171,8 +1196,9 @@ struct X0Set {
 
   // 1 unless v sits in one of its two home slots: 0 proves membership, 1 means
   // "maybe not a member" (resolve with contains / all_in). The sentinel value itself
-  // always answers 1.
+  // always answers 1. (Exact in bitmap mode.)
   PSG_DEV uint32_t maybe_out01(int32_t v) const {
+    if (bmode) return 1u - bm_in01(v);
     const uint32_t h = slot(v);
     const int32_t t0 = tab[h];
     const int32_t t1 = tab[(h + 1) & (uint32_t)(kSlots - 1)];
@@ -1180,6 +1206,7 @@ struct X0Set {
   }
   // contains() as a VALU 0/1 integer (see nz01); same probing scheme
   PSG_DEV uint32_t contains01(int32_t v) const {
+    if (bmode) return bm_in01(v);
     const uint32_t h = slot(v);
     const int32_t t0 = tab[h];
     const int32_t t1 = tab[(h + 1) & (uint32_t)(kSlots - 1)];
@@ -1203,6 +1230,7 @@ struct X0Set {
   // Two adjacent slots are read unconditionally (load <= 1/2: almost every probe
   // resolves there); the probe loop runs only if some lane is still unresolved.
   PSG_DEV bool contains(int32_t v) const {
+    if (bmode) return bm_in01(v) != 0u;
     const uint32_t h = slot(v);
     const int32_t t0 = tab[h];
     const int32_t t1 = tab[(h + 1) & (uint32_t)(kSlots - 1)];
