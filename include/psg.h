@@ -292,6 +292,20 @@ int psg_fetch_instances(psg_ctx* ctx, const uint64_t* ids, size_t k,
 int psg_run_batch_spec(psg_ctx* ctx, uint64_t inst_begin, uint64_t inst_count, const psg_spec_program* prog,
                        psg_summary* out, psg_instance_summary* per_inst);
 
+/* Compile a Spec given as Formula text — the S-expression form of the reference's own
+ * Formula trees (psync/formula/Formula.scala: Binding ForAll / Exists / Comprehension,
+ * Application, Variable, Literal), as integration/scala/GpuSpec.scala writes it from a
+ * psync.Spec; format in round_amd/formula.py ("Formula text") — into *out for
+ * psg_run_batch_spec. Replaces, for concrete checking, the Verifier's assembly of the
+ * Spec (psync/verification/Verifier.scala:111-141). Host code, no device needed.
+ * alg (enum psg_alg, 0 = unchecked) restricts the fields to the algorithm's state and is
+ * recorded in out->alg. The arrays are the library's: release them with psg_spec_release.
+ * names (nullable) receives the slot names, '\n'-separated ("Safety", "Invariant0", ...,
+ * the property names, "SafetyPredicate"); err (nullable) the reason of a failure. */
+int psg_spec_from_text(const char* text, int32_t alg, psg_spec_program* out, char* names, size_t names_len,
+                       char* err, size_t err_len);
+void psg_spec_release(psg_spec_program* prog);
+
 /* Real-valued algorithms (PSG_ALG_EPSILON, RealConsensusIO, Epsilon.scala:10-13).
  * Same contracts as the int32 entry points; other algorithms get PSG_EINVAL.
  * host_init: [count][n] Double initial values, NULL = seeded (uniform [0,1)). */

@@ -46,6 +46,151 @@ PSG_DEV void benor_check(Grp<W>& g, Checks& ck, int c, bool has_old, int n, cons
   ck.record(fb, meq(D, full), c, g.lane);
 }
 
+// ---------------------------------------------------------------- one exchange per round
+// The built-in checker and the round step share ONE cross-wave exchange per round
+// (the general path below pays four: the round's alive ballot, its pre-state
+// ballots and two for the Spec check). At check point c each wave publishes
+//   - a summary word: its popcounts of x and of decided, and one "some process"
+//     flag per quantified witness of the Spec, plus the SafetyPredicate witness
+//     (|HO(p)| <= n/2 on the effective sets) of the round just executed;
+//   - the masks the next round's mailbox statistics need: alive, and x / canDecide
+//     (next round R0) or vote == Some(true) / Some(false) (next round R1).
+// The Spec is evaluated as benor_check does; its roundInvariant witness "vote defined
+// and |{i : i.x == vote.get}| <= n/2" is "(|x| <= n/2 and some vote is Some(true)) or
+// (|!x| <= n/2 and some vote is Some(false))", |x| being the same for every process.
+template <int W>
+struct BoXch {
+  uint64_t sum[W];   // popc(x) | popc(decided) << 16 | witness flags << 32, per wave
+  uint64_t m[3][W];  // alive, x or vote == 1, canDecide or vote == 0
+};
+
+template <int W, class SC>
+PSG_DEV void benor_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashSets<W>& cs, BoXch<W> (&X)[2],
+                        int32_t x0, BlockCounters* bc) {
+  const int n = a.n;
+  const int thr = a.variant == 1 ? n / 4 : n / 2;  // BenOr.scala:68, 71 (variant 1: mutation)
+  bool x = x0 != 0, cd = false, decided = false, decision = false, halted = false;
+  int vote = -1;  // Option[Boolean]: -1 None, 0 Some(false), 1 Some(true)
+  bool old_decided = false, old_decision = false;
+  bool predw = false;  // this process broke the SafetyPredicate in the round just executed
+  int32_t dec_val = 0, dec_round = -1, halt_round = -1;
+  Checks ck;
+  ck.reset();
+  Mask<W> act, T1, T2;  // the next round's alive set and payload masks
+  auto check = [&](int c, bool has_old) {
+    const bool r0next = (c & 1) == 0;  // round c is an R0
+    const bool fl[9] = {decided || cd, (decided && decision) || vote == 1, (decided && !decision) || vote == 0,
+                        decided && decision, decided && !decision, vote == 1, vote == 0,
+                        has_old && old_decided && !(decided && old_decision == decision), predw};
+    uint32_t flags = 0;
+#pragma unroll
+    for (int b = 0; b < 9; ++b) flags |= (__builtin_amdgcn_ballot_w64(g.valid && fl[b]) != 0ull) ? 1u << b : 0u;
+    const uint64_t bx = __builtin_amdgcn_ballot_w64(g.valid && x);
+    const uint64_t bd = __builtin_amdgcn_ballot_w64(g.valid && decided);
+    const uint64_t mw[3] = {__builtin_amdgcn_ballot_w64(g.valid && !halted),
+                            __builtin_amdgcn_ballot_w64(g.valid && (r0next ? x : vote == 1)),
+                            __builtin_amdgcn_ballot_w64(g.valid && (r0next ? cd : vote == 0))};
+    int cntT = __popcll(bx), cntD = __popcll(bd);
+    if constexpr (W == 1) {
+      act.w[0] = mw[0];
+      T1.w[0] = mw[1];
+      T2.w[0] = mw[2];
+    } else {
+      BoXch<W>& e = X[c & 1];
+      if (g.lane == 0) {
+        e.sum[g.wv] = (uint64_t)cntT | ((uint64_t)cntD << 16) | ((uint64_t)flags << 32);
+        e.m[0][g.wv] = mw[0];
+        e.m[1][g.wv] = mw[1];
+        e.m[2][g.wv] = mw[2];
+      }
+      __syncthreads();
+      cntT = 0;
+      cntD = 0;
+      flags = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const uint64_t sw = rfl64(e.sum[w]);
+        cntT += (int)(sw & 0xFFFFu);
+        cntD += (int)((sw >> 16) & 0xFFFFu);
+        flags |= (uint32_t)(sw >> 32);
+        act.w[w] = rfl64(e.m[0][w]);
+        T1.w[w] = rfl64(e.m[1][w]);
+        T2.w[w] = rfl64(e.m[2][w]);
+      }
+    }
+    const int cntF = n - cntT;
+    const bool noDec = !(flags & 1u);
+    const bool ex = (cntF > n / 2 && !(flags & 2u)) || (cntT > n / 2 && !(flags & 4u));
+    const bool rfail = (c & 1) != 0 && ((!(cntT > n / 2) && (flags & 32u)) || (!(cntF > n / 2) && (flags & 64u)));
+    const bool inv0 = (noDec || ex) && !rfail;
+    const bool same = !((flags & 8u) && (flags & 16u));
+    const bool irrev = !(flags & 128u);
+    const bool pred = !(flags & 256u);
+    ck.record(fbit(inv0, 0) | fbit(inv0, 1) | fbit(same, 2) | fbit(irrev, 3) | fbit(pred, 4), cntD == n, c, g.lane);
+  };
+  check(0, false);
+  for (int k = 0; k < a.R; ++k) {
+    old_decided = decided;
+    old_decision = decision;
+    predw = false;
+    if (many(act)) {
+      Mask<W> goodS;
+      const bool good = sc.good_round(k, g.lane, a.R, goodS);
+      Mask<W> CB = mzero<W>(), CN = mzero<W>();
+      if (sc.crash_on) cs.sets(g, k, CB, CN);
+      const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+      const int size = mpopc(M);
+      predw = !halted && size <= n / 2;
+      if ((k & 1) == 0) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
+        const Mask<W> Tm = mand(T1, act);
+        const Mask<W> CDm = mand(T2, act);
+        if (!halted) {
+          if (cd) {
+            dec_val = x ? 1 : 0;
+            dec_round = k;
+            decided = true;
+            decision = x;
+            halt_round = k;
+          } else {
+            const Mask<W> MT = mand(M, Tm);
+            const int cT = mpopc(MT);
+            const int cF = size - cT;
+            const bool exT = many(mand(MT, CDm));
+            const bool exF = many(mand(mandn(M, Tm), CDm));
+            if (cT > n / 2 || exT) vote = 1;
+            else if (cF > n / 2 || exF) vote = 0;
+            else vote = -1;
+            cd = many(mand(M, CDm));
+          }
+        }
+      } else {  // R1: broadcast vote — BenOr.scala:57-79
+        const Mask<W> VT = mand(T1, act);
+        const Mask<W> VF = mand(T2, act);
+        if (!halted) {
+          const int t = mpopc(mand(M, VT));
+          const int f = mpopc(mand(M, VF));
+          if (t > thr) {
+            x = true;
+            cd = true;
+          } else if (f > thr) {
+            x = false;
+            cd = true;
+          } else if (t > 1) {
+            x = true;
+          } else if (f > 1) {
+            x = false;
+          } else {
+            x = sc.coin(k, g.pid);
+          }
+        }
+      }
+      if (halt_round == k) halted = true;
+    }
+    check(k + 1, true);
+  }
+  finish_instance<W>(g, a, i, ck, 5, dec_val, dec_round, halt_round, x ? 1 : 0, bc);
+}
+
 // Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
 // fused Spec module (round_amd/formula.py compile_native(fused=True)).
 template <int W, bool XHO, class SH = NoHook>
@@ -54,6 +199,7 @@ PSG_DEV void benor_body(const KArgs& a) {
   __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int32_t crl[W > 1 ? 64 * W : 1];
   __shared__ int64_t red[2 * W];
+  __shared__ BoXch<W> BX[2];
   counters_init(&bc);
   __syncthreads();
   Grp<W> g;
@@ -75,6 +221,12 @@ PSG_DEV void benor_body(const KArgs& a) {
     sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
     if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_BENOR);
+    if constexpr (!SH::kFused) {
+      if (a.trace == nullptr) {  // built-in checker: one exchange per round
+        benor_fast<W>(g, a, i, sc, cs, BX, x0, &bc);
+        continue;
+      }
+    }
     // BenOrProcess state after init(io) (BenOr.scala:13-28); vote starts as None
     bool x = x0 != 0, cd = false, decided = false, decision = false, halted = false;
     int vote = -1;  // Option[Boolean]: -1 None, 0 Some(false), 1 Some(true)

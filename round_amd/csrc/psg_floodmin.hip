@@ -17,6 +17,142 @@ struct FmLds {
   int32_t ds[W > 1 ? 64 * W : 1];
 };
 
+// ---------------------------------------------------------------- crash-stop fast path
+// Seeded crash-stop schedules without benign loss, good rounds or ho_min (the C4
+// family): HO(p, k) = all \ (CB_k | (CN_k \ S_p)), where CB_k = crashed before k,
+// CN_k = crashing in k and S_p = the senders whose crash-round message reaches p
+// (p's survival words), plus p itself. So FloodMin's update (FloodMin.scala:25-31)
+//   x(p) = min(x(p), min{x_q : q in HO(p) & alive})
+// is min(x(p), m_U, min{x_q : q in CN_k & alive & S_p}) with m_U the group minimum
+// over U = alive \ (CB_k | CN_k): one group reduction, plus a per-receiver pass over
+// the (few) processes crashing in round k. The group minimum over U_{k+1} rides on
+// the exchange of the Spec check after round k, with the check's ballots (decided,
+// decided-and-correct, decided-a-non-initial-value, alive) and the minimum and
+// maximum decision of the correct deciders (k-agreement with k = 1: at most one
+// value iff min == max): one block barrier per round, where the general path pays
+// one per min-loop step and per exchange.
+template <int W>
+struct FmXch {  // one wave's part of a round's exchange
+  uint64_t b[4];       // ballot words: decided, decided & correct, decided & non-initial, alive
+  int32_t mu, dmn, dmx, pad;
+};
+
+template <int W>
+struct FmFast {
+  FmXch<W> ex[2][W];
+  int32_t xs[2][64 * W];  // x after the last round, by check parity (the crash-round senders' values)
+};
+
+template <int W, class SC>
+PSG_DEV void floodmin_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashSets<W>& cs, FmFast<W>& F,
+                           const X0Set<W>& X0, int32_t x0, BlockCounters* bc) {
+  const int n = a.n, f = a.param;
+  const Mask<W> full = mfull<W>(n);
+  const int32_t mycr = g.valid ? sc.crash_round : -1;
+  const bool crashed = mycr >= 0;
+  int32_t x = x0, decision = 0;
+  bool decided = false, halted = false;
+  int32_t dec_val = 0, dec_round = -1, halt_round = -1;
+  Checks ck;
+  ck.reset();
+  int32_t mU = INT32_MAX;  // group minimum of x over U of the next round
+  Mask<W> act = mzero<W>();
+  // check point c (after round c - 1) + the exchange for round c
+  auto check = [&](int c) {
+    const int par = c & 1;
+    const bool alive = g.valid && !halted;
+    const bool inU = alive && !(mycr >= 0 && mycr <= c);  // not crashed before or in round c
+    const bool dc = g.valid && decided && !crashed;
+    const uint64_t b0 = __builtin_amdgcn_ballot_w64(g.valid && decided);
+    const uint64_t b1 = __builtin_amdgcn_ballot_w64(g.valid && dc);
+    const uint64_t b2 = __builtin_amdgcn_ballot_w64(g.valid && decided && !X0.contains(decision));
+    const uint64_t b3 = __builtin_amdgcn_ballot_w64(alive);
+    const int32_t wmu = g.wave_min32(inU ? x : INT32_MAX);
+    const int32_t wmn = g.wave_min32(dc ? decision : INT32_MAX);
+    const int32_t wmx = g.wave_max32(dc ? decision : INT32_MIN);
+    Mask<W> D, Y, BAD;
+    int32_t dmn, dmx;
+    if constexpr (W == 1) {
+      D.w[0] = b0;
+      Y.w[0] = b1;
+      BAD.w[0] = b2;
+      act.w[0] = b3;
+      mU = wmu;
+      dmn = wmn;
+      dmx = wmx;
+    } else {
+      F.xs[par][g.pid] = x;
+      FmXch<W>& e = F.ex[par][g.wv];
+      if (g.lane == 0) {
+        e.b[0] = b0;
+        e.b[1] = b1;
+        e.b[2] = b2;
+        e.b[3] = b3;
+        e.mu = wmu;
+        e.dmn = wmn;
+        e.dmx = wmx;
+      }
+      __syncthreads();
+      mU = INT32_MAX;
+      dmn = INT32_MAX;
+      dmx = INT32_MIN;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const FmXch<W>& r = F.ex[par][w];
+        D.w[w] = rfl64(r.b[0]);
+        Y.w[w] = rfl64(r.b[1]);
+        BAD.w[w] = rfl64(r.b[2]);
+        act.w[w] = rfl64(r.b[3]);
+        mU = min(mU, rfl32(r.mu));
+        dmn = min(dmn, rfl32(r.dmn));
+        dmx = max(dmx, rfl32(r.dmx));
+      }
+    }
+    const bool one = !many(Y) || dmn == dmx;  // KAgreement with k = 1 (kagree_check)
+    ck.record(fbit(one, 0) | fbit(!many(BAD), 1), meq(D, full), c, g.lane);
+  };
+  check(0);
+  for (int k = 0; k < a.R; ++k) {
+    if (many(act)) {
+      Mask<W> CB, CN;
+      cs.sets(g, k, CB, CN);
+      const Mask<W> CNa = mand(CN, act);
+      int32_t nx = min(x, mU);
+      if (many(CNa)) {  // crash round of some alive sender: its message reaches p iff p's survival bit
+        uint64_t dm[W], hf[W];
+        sc.draw((uint32_t)k, (uint32_t)g.pid, false, true, dm, hf);
+        Mask<W> rem = CNa;
+        while (many(rem)) {
+          const int q = mfirst(rem);
+          mclear(rem, q);
+          int32_t xq;
+          if constexpr (W == 1) xq = readlane32(x, q);
+          else xq = rfl32(F.xs[k & 1][q]);
+          uint64_t word = hf[0];
+#pragma unroll
+          for (int w = 1; w < W; ++w)
+            if ((q >> 6) == w) word = hf[w];
+          if ((word >> (q & 63)) & 1ull) nx = min(nx, xq);
+        }
+      }
+      if (!halted) {
+        x = nx;
+        const bool decideNow = a.variant == 1 ? (k >= f - 1) : (k > f);  // FloodMin.scala:27 (variant 1: mutation)
+        if (decideNow) {
+          dec_val = x;
+          dec_round = k;
+          decided = true;
+          decision = x;
+          halt_round = k;
+          halted = true;
+        }
+      }
+    }
+    check(k + 1);
+  }
+  finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, x, bc);
+}
+
 // Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
 // fused Spec module (round_amd/formula.py compile_native(fused=True)).
 template <int W, bool XHO, class SH = NoHook>
@@ -27,6 +163,7 @@ PSG_DEV void floodmin_body(const KArgs& a) {
   __shared__ int64_t red[2 * W];
   __shared__ FmLds<W> L;
   __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
+  __shared__ FmFast<W> FF;  // crash-stop fast path (W == 1 uses registers only)
   counters_init(&bc);
   __syncthreads();
   Grp<W> g;
@@ -51,6 +188,12 @@ PSG_DEV void floodmin_body(const KArgs& a) {
     if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_FLOODMIN);
     X0Set<W> X0;
     X0.build(g, x0tab[grp], x0);
+    if constexpr (!XHO && !SH::kFused) {
+      if (a.trace == nullptr && a.drop_log2 == 0 && a.good_p32 == 0 && a.ho_min < 0) {
+        floodmin_fast<W>(g, a, i, sc, cs, FF, X0, x0, &bc);
+        continue;
+      }
+    }
     int32_t x = x0, decision = 0;
     bool decided = false, halted = false;
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;

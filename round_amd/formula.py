@@ -1099,3 +1099,286 @@ def compile_native(spec: Spec, alg: Optional[int] = None, cache_dir: str = None,
         os.replace(out + ".tmp", out)
     prog.module_path = out
     return prog
+
+
+# --------------------------------------------------------------------------- Formula text (JVM interchange)
+# A Spec as the S-expression text of the reference's own Formula trees
+# (psync/formula/Formula.scala:20-583: Binding(ForAll | Exists | Comprehension),
+# Application(symbol, args), Variable, Literal), as integration/scala/GpuSpec.scala
+# writes it from a psync.Spec and as psg_spec_from_text (psg_spec_text.cpp, the C ABI)
+# compiles it; `from_text` here gives the same Spec in this DSL (for compile_native).
+#
+#   spec  := (Spec (phase L) (invariants f*) (roundInvariants (list f*)*)
+#                  (properties (prop "Name" f)*) [(safetyPredicate f)])
+#   f     := (ForAll (decl+) f) | (Exists (decl+) f) | (Comprehension (decl) f)
+#          | (App SYMBOL f*) | (Var NAME) | (Lit INT | true | false)
+#   decl  := (NAME pid | Int | Bool | Set)
+#
+# Symbols: the InterpretedFct names And Or Not Implies Eq Neq Lt Leq Gt Geq Plus Minus
+# Times Divides In Contains Cardinality IsDefined IsEmpty Get Some (Formula.scala:175-348;
+# Remainder is this format's `%`), process fields x decided decision ts ready commit vote
+# canDecide est with the `__init__` / `__old__` prefixes of init(...) / old(...)
+# (psync/verification/Utils.scala:24-25), HO (Cardinality(HO(p)) = |HO(p)|) and coord.
+# Variables n and r and coord are the free ones. FormulaExtractor's
+# `val A = P.filter(...); body` arrives as (Exists ((A Set)) (App And (App Eq (Var A)
+# (Comprehension ...)) body...)) and is substituted back.
+FIELD_NAMES = {"x": FIELD_X, "decided": FIELD_DECIDED, "decision": FIELD_DECISION, "ts": FIELD_TS,
+               "ready": FIELD_READY, "commit": FIELD_COMMIT, "vote": FIELD_VOTE, "canDecide": FIELD_CANDECIDE,
+               "est": FIELD_X}
+_FIELD_TEXT = {FIELD_X: "x", FIELD_DECIDED: "decided", FIELD_DECISION: "decision", FIELD_TS: "ts",
+               FIELD_READY: "ready", FIELD_COMMIT: "commit", FIELD_VOTE: "vote", FIELD_CANDECIDE: "canDecide"}
+_BIN_TEXT = {"AND": "And", "OR": "Or", "IMPL": "Implies", "EQ": "Eq", "NE": "Neq", "LT": "Lt", "LE": "Leq",
+             "GT": "Gt", "GE": "Geq", "ADD": "Plus", "SUB": "Minus", "MUL": "Times", "DIV": "Divides",
+             "MOD": "Remainder"}
+_TEXT_BIN = {v: k for k, v in _BIN_TEXT.items()}
+
+
+def _expr_text(e, names) -> str:
+    def nm(v):
+        if v.uid not in names:
+            names[v.uid] = f"{v.kind[0]}{len(names)}"
+        return names[v.uid]
+
+    def t(e):
+        if isinstance(e, Lit):
+            return f"(Lit {e.v})"
+        if isinstance(e, NVal):
+            return "(Var n)"
+        if isinstance(e, RVal):
+            return "(Var r)"
+        if isinstance(e, CoordVal):
+            return "(Var coord)"
+        if isinstance(e, Var):
+            return f"(Var {nm(e)})"
+        if isinstance(e, Field):
+            if e.f == FIELD_HOSIZE:
+                return f"(App Cardinality (App HO {t(e.proc)}))"
+            pre = {TAG_CUR: "", TAG_OLD: "__old__", TAG_INIT: "__init__"}[e.tag]
+            return f"(App {pre}{_FIELD_TEXT[e.f]} {t(e.proc)})"
+        if isinstance(e, Un):
+            op = {"NOT": "Not", "NEG": "Minus", "ISDEF": "IsDefined"}[e.op]
+            return f"(App {op} {t(e.x)})"
+        if isinstance(e, Bin):
+            return f"(App {_BIN_TEXT[e.op]} {t(e.x)} {t(e.y)})"
+        if isinstance(e, Contains):
+            return f"(App In {t(e.e)} {comp(e.comp)})"
+        if isinstance(e, Quant):
+            if e.kind == "count":
+                return f"(App Cardinality (Comprehension (({nm(e.var)} pid)) {t(e.body)}))"
+            typ = {"forall": "pid", "exists": "pid", "vint": "Int", "vbool": "Bool"}[e.kind]
+            b = "ForAll" if e.kind == "forall" else "Exists"
+            return f"({b} (({nm(e.var)} {typ})) {t(e.body)})"
+        raise FormulaError(f"cannot write {type(e).__name__} as Formula text")
+
+    def comp(c):
+        return f"(Comprehension (({nm(c.var)} pid)) {t(c.body)})"
+
+    return t(e)
+
+
+def to_text(spec: Spec) -> str:
+    """The Spec as Formula text (the interchange format above)."""
+    names: Dict[int, str] = {}
+    out = [f"(Spec (phase {spec.phase_length})"]
+    out.append("  (invariants " + " ".join(_expr_text(f, names) for f in spec.invariants) + ")")
+    out.append("  (roundInvariants " + " ".join(
+        "(list " + " ".join(_expr_text(f, names) for f in l) + ")" for l in spec.round_invariants) + ")")
+    out.append("  (properties " + " ".join(f'(prop "{nm}" {_expr_text(f, names)})' for nm, f in spec.properties)
+               + ")")
+    if spec.safety_predicate is not None:
+        out.append("  (safetyPredicate " + _expr_text(spec.safety_predicate, names) + ")")
+    return "\n".join(out) + ")"
+
+
+def _sexp(text: str):
+    toks, i = [], 0
+    while i < len(text):
+        ch = text[i]
+        if ch.isspace():
+            i += 1
+        elif ch in "()":
+            toks.append(ch)
+            i += 1
+        elif ch == '"':
+            j = text.index('"', i + 1)
+            toks.append(("str", text[i + 1:j]))
+            i = j + 1
+        else:
+            j = i
+            while j < len(text) and not text[j].isspace() and text[j] not in '()"':
+                j += 1
+            toks.append(text[i:j])
+            i = j
+    pos = 0
+
+    def parse():
+        nonlocal pos
+        if pos >= len(toks):
+            raise FormulaError("Formula text: unexpected end")
+        tk = toks[pos]
+        pos += 1
+        if tk == "(":
+            lst = []
+            while pos < len(toks) and toks[pos] != ")":
+                lst.append(parse())
+            if pos >= len(toks):
+                raise FormulaError("Formula text: missing )")
+            pos += 1
+            return lst
+        if tk == ")":
+            raise FormulaError("Formula text: unexpected )")
+        return tk
+
+    v = parse()
+    if pos != len(toks):
+        raise FormulaError("Formula text: trailing input")
+    return v
+
+
+def _from_sexp(s, env):
+    if not isinstance(s, list) or not s:
+        raise FormulaError(f"Formula text: expected a form, got {s!r}")
+    head = s[0]
+    if head == "Lit":
+        v = s[1]
+        return Lit(1 if v == "true" else 0 if v == "false" else int(v))
+    if head == "Var":
+        name = s[1]
+        if name in env:
+            return env[name]
+        if name == "n":
+            return NVal()
+        if name == "r":
+            return RVal()
+        if name == "coord":
+            return CoordVal()
+        raise FormulaError(f"Formula text: unbound variable {name}")
+    if head in ("ForAll", "Exists"):
+        decls, body = s[1], s[2]
+        if not decls:
+            raise FormulaError("Formula text: binder without variables")
+        (name, typ), rest = decls[0], decls[1:]
+        inner = [head, rest, body] if rest else body
+        if typ == "Set":  # FormulaExtractor's `val A = ...; body`
+            if head != "Exists":
+                raise FormulaError("Formula text: a Set variable is only bound by a let (Exists)")
+            return _let(name, inner, env)
+        if typ == "pid":
+            v = Var("proc")
+            return Quant("forall" if head == "ForAll" else "exists", v, _from_sexp(inner, {**env, name: v}))
+        if head == "ForAll":
+            raise FormulaError(f"Formula text: ForAll over {typ} cannot be checked (only V.exists)")
+        v = Var("int" if typ == "Int" else "bool")
+        return Quant("vint" if typ == "Int" else "vbool", v, _from_sexp(inner, {**env, name: v}))
+    if head == "Comprehension":
+        return _comp(s, env)
+    if head == "App":
+        sym, args = s[1], s[2:]
+        a = lambda k: _from_sexp(args[k], env)  # noqa: E731
+        if sym in ("And", "Or"):
+            out = a(0)
+            for k in range(1, len(args)):
+                out = Bin(sym.upper(), out, a(k))
+            return out
+        if sym in _TEXT_BIN:
+            if sym == "Minus" and len(args) == 1:
+                return Un("NEG", a(0))
+            return Bin(_TEXT_BIN[sym], a(0), a(1))
+        if sym == "Not":
+            return Un("NOT", a(0))
+        if sym == "IsDefined":
+            return Un("ISDEF", a(0))
+        if sym == "IsEmpty":
+            return Un("NOT", Un("ISDEF", a(0)))
+        if sym in ("Get", "Some"):
+            return a(0)
+        if sym == "Cardinality":
+            x = args[0]
+            if isinstance(x, list) and x and x[0] == "App" and x[1] == "HO":
+                return Field(FIELD_HOSIZE, _from_sexp(x[2], env))
+            c = _set(x, env)
+            return c.size
+        if sym in ("In", "Contains"):
+            elem, st = (args[0], args[1]) if sym == "In" else (args[1], args[0])
+            return _set(st, env).contains(_from_sexp(elem, env))
+        if sym == "coord" and not args:
+            return CoordVal()
+        tag, base = TAG_CUR, sym
+        if sym.startswith("__init__"):
+            tag, base = TAG_INIT, sym[len("__init__"):]
+        elif sym.startswith("__old__"):
+            tag, base = TAG_OLD, sym[len("__old__"):]
+        if base in FIELD_NAMES and len(args) == 1:
+            return Field(FIELD_NAMES[base], a(0), tag)
+        raise FormulaError(f"Formula text: unknown symbol {sym}/{len(args)}")
+    raise FormulaError(f"Formula text: unknown form {head}")
+
+
+def _comp(s, env):
+    (name, typ), = s[1]
+    if typ != "pid":
+        raise FormulaError("Formula text: comprehensions range over processes")
+    v = Var("proc")
+    return Comprehension(v, _from_sexp(s[2], {**env, name: v}))
+
+
+def _set(s, env):
+    if isinstance(s, list) and s and s[0] == "Comprehension":
+        return _comp(s, env)
+    if isinstance(s, list) and s and s[0] == "Var" and isinstance(env.get(s[1]), Comprehension):
+        return env[s[1]]
+    raise FormulaError("Formula text: expected a set of processes")
+
+
+def _let(name, body, env):
+    """Exists A: Set. A == {..} && rest  ->  rest with A := {..}."""
+    conj = []
+
+    def flat(x):
+        if isinstance(x, list) and len(x) >= 3 and x[0] == "App" and x[1] == "And":
+            for y in x[2:]:
+                flat(y)
+        else:
+            conj.append(x)
+
+    flat(body)
+    for k, c in enumerate(conj):
+        if isinstance(c, list) and len(c) == 4 and c[0] == "App" and c[1] == "Eq":
+            for lhs, rhs in ((c[2], c[3]), (c[3], c[2])):
+                if lhs == ["Var", name] and isinstance(rhs, list) and rhs and rhs[0] == "Comprehension":
+                    rest = conj[:k] + conj[k + 1:]
+                    if not rest:
+                        return Lit(1)
+                    env2 = {**env, name: _comp(rhs, env)}
+                    return _from_sexp(rest[0] if len(rest) == 1 else ["App", "And"] + rest, env2)
+    raise FormulaError(f"Formula text: Set variable {name} is not defined by a conjunct {name} == {{...}}")
+
+
+def from_text(text: str) -> Spec:
+    """Parse Formula text (the interchange format above) into a Spec."""
+    s = _sexp(text)
+    if not (isinstance(s, list) and s and s[0] == "Spec"):
+        raise FormulaError("Formula text: expected (Spec ...)")
+    phase, invs, rinv, props, sp = 1, [], [], [], None
+    for part in s[1:]:
+        key = part[0]
+        if key == "phase":
+            phase = int(part[1])
+        elif key == "invariants":
+            invs = [_from_sexp(f, {}) for f in part[1:]]
+        elif key == "roundInvariants":
+            rinv = [[_from_sexp(f, {}) for f in l[1:]] for l in part[1:]]
+        elif key == "properties":
+            props = [(p[1][1], _from_sexp(p[2], {})) for p in part[1:]]
+        elif key == "safetyPredicate":
+            sp = _from_sexp(part[1], {})
+        else:
+            raise FormulaError(f"Formula text: unknown Spec part {key}")
+    return Spec(invs, rinv, props, safety_predicate=sp, phase_length=phase)
+
+
+def compile_text(text: str, alg: Optional[int] = None) -> Program:
+    """Formula text -> bytecode Program through the C ABI (psg_spec_from_text in libpsg),
+    the path the JVM plugin takes; equal to compile_spec(from_text(text), alg)."""
+    from . import lib
+    return lib.spec_from_text(text, alg or 0)
