@@ -50,6 +50,9 @@ struct JNINativeInterface_ {
   void (*GetIntArrayRegion)(JNIEnv* env, jintArray array, jsize start, jsize len, jint* buf);
   void (*SetByteArrayRegion)(JNIEnv* env, jbyteArray array, jsize start, jsize len, const jbyte* buf);
   void (*SetLongArrayRegion)(JNIEnv* env, jlongArray array, jsize start, jsize len, const jlong* buf);
+  jintArray (*NewIntArray)(JNIEnv* env, jsize len);
+  void (*SetIntArrayRegion)(JNIEnv* env, jintArray array, jsize start, jsize len, const jint* buf);
+  jstring (*NewStringUTF)(JNIEnv* env, const char* utf);
   const char* (*GetStringUTFChars)(JNIEnv* env, jstring str, jboolean* isCopy);
   void (*ReleaseStringUTFChars)(JNIEnv* env, jstring str, const char* chars);
 };

@@ -246,6 +246,60 @@ JNIEXPORT jlongArray JNICALL Java_psync_gpu_GpuRoundNative_00024_runBatchSpec(
   return summary_array(env, &s);
 }
 
+/* int[] compileSpec(String text, int alg) — psg_spec_from_text: the Formula text of a Spec
+ * (integration/scala/GpuSpec.scala) compiled to bytecode, returned packed as
+ * [nSlots, nWords, termEntry, nVars, code[nWords], slotEntry[nSlots], slotFlags[nSlots]]. */
+JNIEXPORT jintArray JNICALL Java_psync_gpu_GpuRoundNative_00024_compileSpec(JNIEnv* env, jobject self, jstring text,
+                                                                            jint alg) {
+  (void)self;
+  if (!text) {
+    throw_cls(env, "java/lang/IllegalArgumentException", "text must not be null");
+    return NULL;
+  }
+  const char* t = (*env)->GetStringUTFChars(env, text, NULL);
+  psg_spec_program p;
+  char err[512];
+  const int rc = psg_spec_from_text(t, alg, &p, NULL, 0, err, sizeof err);
+  (*env)->ReleaseStringUTFChars(env, text, t);
+  if (rc) {
+    throw_psg(env, rc, err);
+    return NULL;
+  }
+  const jsize len = 4 + p.n_words + 2 * p.n_slots;
+  jintArray out = (*env)->NewIntArray(env, len);
+  if (out) {
+    const jint head[4] = {p.n_slots, p.n_words, p.term_entry, p.n_vars};
+    (*env)->SetIntArrayRegion(env, out, 0, 4, head);
+    (*env)->SetIntArrayRegion(env, out, 4, p.n_words, (const jint*)p.code);
+    (*env)->SetIntArrayRegion(env, out, 4 + p.n_words, p.n_slots, (const jint*)p.slot_entry);
+    (*env)->SetIntArrayRegion(env, out, 4 + p.n_words + p.n_slots, p.n_slots, (const jint*)p.slot_flags);
+  }
+  psg_spec_release(&p);
+  return out;
+}
+
+/* String compileSpecNames(String text, int alg) — the slot names of compileSpec's program,
+ * '\n'-separated ("Safety", "Invariant0", ..., property names, "SafetyPredicate"). */
+JNIEXPORT jstring JNICALL Java_psync_gpu_GpuRoundNative_00024_compileSpecNames(JNIEnv* env, jobject self,
+                                                                               jstring text, jint alg) {
+  (void)self;
+  if (!text) {
+    throw_cls(env, "java/lang/IllegalArgumentException", "text must not be null");
+    return NULL;
+  }
+  const char* t = (*env)->GetStringUTFChars(env, text, NULL);
+  psg_spec_program p;
+  char names[4096], err[512];
+  const int rc = psg_spec_from_text(t, alg, &p, names, sizeof names, err, sizeof err);
+  (*env)->ReleaseStringUTFChars(env, text, t);
+  if (rc) {
+    throw_psg(env, rc, err);
+    return NULL;
+  }
+  psg_spec_release(&p);
+  return (*env)->NewStringUTF(env, names);
+}
+
 /* void copyDecisions(long ctx, int[] decision, int[] decisionRound) — the batched
  * ConsensusIO.decide results of the last batch, [count][n] each (either may be null). */
 JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_copyDecisions(JNIEnv* env, jobject self, jlong h,

@@ -223,7 +223,8 @@ struct Lower {
     if (sym == "Not" && na == 1) return T.un(PSG_OP_NOT, arg(0));
     if (sym == "IsDefined" && na == 1) return T.un(PSG_OP_ISDEF, arg(0));
     if (sym == "IsEmpty" && na == 1) return T.un(PSG_OP_NOT, T.un(PSG_OP_ISDEF, arg(0)));
-    if ((sym == "Get" || sym == "Some") && na == 1) return arg(0);
+    // Option get / Some; Time <-> Int conversions of psync.logic.ReduceTime (identities here)
+    if ((sym == "Get" || sym == "Some" || sym == "toInt" || sym == "fromInt") && na == 1) return arg(0);
     if (sym == "Cardinality" && na == 1) {
       const Sx& x = s.at(2);
       if (x.is("App") && x.items.size() == 3 && x.at(1).atom && x.at(1).tok == "HO") {
@@ -282,8 +283,8 @@ struct Lower {
     e2[nm] = Binding{false, uid, {}};
     if (typ == "pid") return T.quant(forall ? QFORALL : QEXISTS, uid, inner(e2));
     if (forall) throw SpecError("Formula text: ForAll over " + typ + " cannot be checked (only V.exists)");
-    if (typ != "Int" && typ != "Bool") throw SpecError("Formula text: unknown type " + typ);
-    return T.quant(typ == "Int" ? QVINT : QVBOOL, uid, inner(e2));
+    if (typ != "Int" && typ != "Time" && typ != "Bool") throw SpecError("Formula text: unknown type " + typ);
+    return T.quant(typ == "Bool" ? QVBOOL : QVINT, uid, inner(e2));
   }
 
   Comp comp(const Sx& s, const Env& env) {

@@ -1112,11 +1112,12 @@ def compile_native(spec: Spec, alg: Optional[int] = None, cache_dir: str = None,
 #                  (properties (prop "Name" f)*) [(safetyPredicate f)])
 #   f     := (ForAll (decl+) f) | (Exists (decl+) f) | (Comprehension (decl) f)
 #          | (App SYMBOL f*) | (Var NAME) | (Lit INT | true | false)
-#   decl  := (NAME pid | Int | Bool | Set)
+#   decl  := (NAME pid | Int | Time | Bool | Set)       (Time: the round type, read as Int)
 #
 # Symbols: the InterpretedFct names And Or Not Implies Eq Neq Lt Leq Gt Geq Plus Minus
 # Times Divides In Contains Cardinality IsDefined IsEmpty Get Some (Formula.scala:175-348;
-# Remainder is this format's `%`), process fields x decided decision ts ready commit vote
+# Remainder is this format's `%`), toInt / fromInt (psync.logic.ReduceTime, Time <-> Int,
+# identities here), process fields x decided decision ts ready commit vote
 # canDecide est with the `__init__` / `__old__` prefixes of init(...) / old(...)
 # (psync/verification/Utils.scala:24-25), HO (Cardinality(HO(p)) = |HO(p)|) and coord.
 # Variables n and r and coord are the free ones. FormulaExtractor's
@@ -1268,8 +1269,10 @@ def _from_sexp(s, env):
             return Quant("forall" if head == "ForAll" else "exists", v, _from_sexp(inner, {**env, name: v}))
         if head == "ForAll":
             raise FormulaError(f"Formula text: ForAll over {typ} cannot be checked (only V.exists)")
-        v = Var("int" if typ == "Int" else "bool")
-        return Quant("vint" if typ == "Int" else "vbool", v, _from_sexp(inner, {**env, name: v}))
+        if typ not in ("Int", "Time", "Bool"):
+            raise FormulaError(f"Formula text: unknown type {typ}")
+        v = Var("bool" if typ == "Bool" else "int")
+        return Quant("vbool" if typ == "Bool" else "vint", v, _from_sexp(inner, {**env, name: v}))
     if head == "Comprehension":
         return _comp(s, env)
     if head == "App":
@@ -1290,7 +1293,7 @@ def _from_sexp(s, env):
             return Un("ISDEF", a(0))
         if sym == "IsEmpty":
             return Un("NOT", Un("ISDEF", a(0)))
-        if sym in ("Get", "Some"):
+        if sym in ("Get", "Some", "toInt", "fromInt"):  # Option get / Some; Time <-> Int (ReduceTime)
             return a(0)
         if sym == "Cardinality":
             x = args[0]

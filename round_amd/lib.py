@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = [
     "psg_fetch_instances", "psg_last_error", "psg_destroy", "psg_create_error",
     "psg_selftest_map_head", "psg_load_inputs_f64", "psg_copy_decisions_f64", "psg_fetch_instances_f64",
     "psg_run_batch_spec", "psg_load_schedule", "psg_clear_schedule", "psg_materialize_schedule",
-    "psg_population_fresh", "psg_population_next", "psg_population_read",
+    "psg_population_fresh", "psg_population_next", "psg_population_read", "psg_spec_from_text", "psg_spec_release",
 ]
 
 
@@ -75,6 +75,10 @@ def load():
     L.psg_population_fresh.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(abi.PopulationParams)]
     L.psg_population_next.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(abi.PopulationParams)]
     L.psg_population_read.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
+    L.psg_spec_from_text.argtypes = [C.c_char_p, C.c_int32, C.POINTER(abi.SpecProgram), C.c_char_p, C.c_size_t,
+                                     C.c_char_p, C.c_size_t]
+    L.psg_spec_release.argtypes = [C.POINTER(abi.SpecProgram)]
+    L.psg_spec_release.restype = None
     L.psg_selftest_map_head.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
                                         C.POINTER(C.c_int32)]
     _lib = L
@@ -309,3 +313,25 @@ def selftest_map_head(sets, tiebreak=abi.PSG_TIE_CHAMP, device=0):
     if rc != 0:
         raise PsgError(rc, "psg_selftest_map_head failed")
     return list(out)[:k]
+
+
+def spec_from_text(text, alg=0):
+    """psg_spec_from_text (host code, no GPU): Formula text -> formula.Program (bytecode).
+    Raises formula.FormulaError with the library's message on a rejected text."""
+    from . import formula
+    L = load()
+    cp = abi.SpecProgram()
+    names = C.create_string_buffer(4096)
+    err = C.create_string_buffer(1024)
+    rc = L.psg_spec_from_text(text.encode(), int(alg), C.byref(cp), names, len(names), err, len(err))
+    if rc != 0:
+        raise formula.FormulaError(err.value.decode() or f"psg_spec_from_text rc={rc}")
+    try:
+        code = [cp.code[k] for k in range(cp.n_words)]
+        entry = [cp.slot_entry[k] for k in range(cp.n_slots)]
+        flags = [cp.slot_flags[k] for k in range(cp.n_slots)]
+        prog = formula.Program(code, entry, flags, cp.term_entry, cp.n_vars, names.value.decode().split("\n"), None)
+        prog.alg = cp.alg
+        return prog
+    finally:
+        L.psg_spec_release(C.byref(cp))
