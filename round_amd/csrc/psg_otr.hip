@@ -53,8 +53,22 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
   if constexpr (!V2) wit = (wit & dec01) | X0.maybe_out01(x);  // keepInit (OTR only)
   else wit &= dec01;
   if (has_old) wit |= old01 & (1u - (dec01 & eq01(old_decision, decision)));
+  const bool term = meq(D, full);
+  const bool wany = g.any((wit & valid01) != 0u);
+  if (term && !wany) {
+    // Settled state (every process decided, no witness): keepInit, Validity, Agreement
+    // and Irrevocability hold, so Invariant2 (OTR: term && all decisions equal and
+    // initial; OTR2: all decisions equal), Safety and Integrity hold; Invariant0 reduces
+    // to e0 (OTR2: term), Invariant1 to e1, with the vote count taken at v = d0. The
+    // same values as the general path below, in a few scalar instructions (most check
+    // points of a run are in this state).
+    const int cnt = mpopc(g.ballot((valid01 & eq01(x, d0)) != 0u));
+    const uint32_t fb = (V2 ? 0u : fbit(cnt > sthr, 1)) | fbit(cnt == n, 2);
+    ck.record(fb, true, c, g.lane);
+    return;
+  }
   bool keep = true, validity = true, same = true, irrev = true;
-  if (g.any((wit & valid01) != 0u)) {  // exact resolution, one ballot per formula
+  if (wany) {  // exact resolution, one ballot per formula
     if constexpr (!V2) keep = X0.all_in(g, full, x);
     validity = X0.all_in(g, D, decision);
     same = !many(mand(D, g.ballot(decision != d0)));
@@ -65,7 +79,6 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
   const bool condv = !anyD || same;
   const bool e0 = condv && cnt > sthr;
   const bool e1 = condv && cnt == n;
-  const bool term = meq(D, full);
   const bool d0in = same && validity;  // all decisions equal d0 and are initial values
   // OTR: Otr.scala:99-110; OTR2: Otr2.scala:75-87
   const bool inv0 = V2 ? (term || e0) : ((!anyD || e0) && keep);
