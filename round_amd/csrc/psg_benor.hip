@@ -1,6 +1,6 @@
 // psg_benor.hip — Ben-Or randomized binary consensus on gfx950.
 //
-// Reference: example/BenOr.scala:11-84 (BenOrProcess), 266-295 (spec).
+// Reference: example/BenOr.scala:11-84 (BenOrProcess), 91-115 (spec).
 // Payloads are one or two bits per process, so every mailbox statistic is a
 // popcount of HO(p) & alive & ballot(bit). The unseeded coin
 // `util.Random.nextBoolean` (BenOr.scala:77) is java.util.Random's first
@@ -8,6 +8,7 @@
 // n = 128 runs as W = 2 waves per instance with the ballot words exchanged in LDS.
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
+#include "psg_packed.hpp"
 
 namespace psg {
 
@@ -191,6 +192,169 @@ PSG_DEV void benor_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashSets
   finish_instance<W>(g, a, i, ck, 5, dec_val, dec_round, halt_round, x ? 1 : 0, bc);
 }
 
+// ---------------------------------------------------------------- built-in checker, lane-packed
+// benor_fast for n > 64 with one wave per instance, the W processes l + 64 j in lane l
+// (psg_packed.hpp): the Spec's existential witnesses are one wave OR of a per-lane flag
+// word (the lane's OR over its slots), the counts and the next round's payload masks
+// are wave ballots, and no round needs a barrier.
+#ifndef PSG_BO_FLAGS_DPP
+#define PSG_BO_FLAGS_DPP 1
+#endif
+template <int W>
+PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, BlockCounters* bc) {
+  const int n = a.n;
+  const int thr = a.variant == 1 ? n / 4 : n / 2;  // BenOr.scala:68, 71 (variant 1: mutation)
+  Sched<W, false> sc;
+  sc.setup(a, inst, P.lane, false);  // uniform parts; crash rounds per slot below
+  sc.prep_good(0, P.lane, a.R);
+  int32_t cr[W];
+  pk_crash_rounds<W>(P, a, inst, cr);
+  // BenOrProcess state after init(io) (BenOr.scala:13-28), 0/1 words per slot
+  uint32_t x[W], cd[W], decided[W], decision[W], halted[W], old_decided[W], old_decision[W], predw[W];
+  int32_t vote[W];  // Option[Boolean]: -1 None, 0 Some(false), 1 Some(true)
+  int32_t dec_val[W], dec_round[W], halt_round[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    int32_t x0 = 0;
+    if (P.val[j])
+      x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + P.pid(j)] : sc.init_value(P.pid(j), PSG_ALG_BENOR);
+    x[j] = x0 != 0 ? 1u : 0u;
+    cd[j] = decided[j] = decision[j] = halted[j] = old_decided[j] = old_decision[j] = predw[j] = 0;
+    vote[j] = -1;
+    dec_val[j] = 0;
+    dec_round[j] = -1;
+    halt_round[j] = -1;
+  }
+  Checks ck;
+  ck.reset();
+  Mask<W> act, T1, T2;  // the next round's alive set and payload masks
+  auto check = [&](int c, bool has_old) {
+    const bool r0next = (c & 1) == 0;  // round c is an R0
+    uint32_t fw = 0;                   // bit b: the Spec witness b holds for some process of the lane
+    uint32_t al[W], t1[W], t2[W], xs[W], ds[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const uint32_t v = P.val[j];
+      const uint32_t v1 = eq01(vote[j], 1), v0 = eq01(vote[j], 0);
+      const uint32_t dT = decided[j] & decision[j], dF = decided[j] & (1u - decision[j]);
+      const uint32_t irr = (has_old ? 1u : 0u) & old_decided[j] & (1u - (decided[j] & eq01((int32_t)old_decision[j], (int32_t)decision[j])));
+      const uint32_t w = (decided[j] | cd[j]) | ((dT | v1) << 1) | ((dF | v0) << 2) | (dT << 3) | (dF << 4) | (v1 << 5) |
+                         (v0 << 6) | (irr << 7) | (predw[j] << 8);
+      fw |= v ? w : 0u;
+      al[j] = v & (1u - halted[j]);
+      t1[j] = v & (r0next ? x[j] : v1);
+      t2[j] = v & (r0next ? cd[j] : v0);
+      xs[j] = v & x[j];
+      ds[j] = v & decided[j];
+    }
+#if PSG_BO_FLAGS_DPP
+    const uint32_t flags = wave_or(fw);
+#else
+    uint32_t flags = 0;
+#pragma unroll
+    for (int b = 0; b < 9; ++b) flags |= pk_any((fw >> b) & 1u) ? 1u << b : 0u;
+#endif
+    act = P.ballot(al);
+    T1 = P.ballot(t1);
+    T2 = P.ballot(t2);
+    const int cntT = mpopc(P.ballot(xs)), cntD = mpopc(P.ballot(ds));
+    const int cntF = n - cntT;
+    const bool noDec = !(flags & 1u);
+    const bool ex = (cntF > n / 2 && !(flags & 2u)) || (cntT > n / 2 && !(flags & 4u));
+    const bool rfail = (c & 1) != 0 && ((!(cntT > n / 2) && (flags & 32u)) || (!(cntF > n / 2) && (flags & 64u)));
+    const bool inv0 = (noDec || ex) && !rfail;
+    const bool same = !((flags & 8u) && (flags & 16u));
+    const bool irrev = !(flags & 128u);
+    const bool pred = !(flags & 256u);
+    ck.record(fbit(inv0, 0) | fbit(inv0, 1) | fbit(same, 2) | fbit(irrev, 3) | fbit(pred, 4), cntD == n, c, P.lane);
+  };
+  check(0, false);
+  for (int k = 0; k < a.R; ++k) {
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      old_decided[j] = decided[j];
+      old_decision[j] = decision[j];
+      predw[j] = 0;
+    }
+    if (many(act)) {
+      Mask<W> goodS;
+      const bool good = sc.good_round(k, P.lane, a.R, goodS);
+      Mask<W> CB = mzero<W>(), CN = mzero<W>();
+      if (sc.crash_on) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          CB.w[j] = __builtin_amdgcn_ballot_w64(cr[j] >= 0 && cr[j] < k);
+          CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
+        }
+      }
+      const bool even = (k & 1) == 0;
+      const Mask<W> A1 = mand(T1, act), A2 = mand(T2, act);  // R0: x / canDecide; R1: vote true / false
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        if (halted[j]) continue;  // a halted process neither receives nor updates
+        const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
+        const int size = mpopc(M);
+        predw[j] = P.val[j] & (size <= n / 2 ? 1u : 0u);
+        if (even) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
+          if (cd[j]) {
+            dec_val[j] = (int32_t)x[j];
+            dec_round[j] = k;
+            decided[j] = 1;
+            decision[j] = x[j];
+            halt_round[j] = k;
+          } else {
+            const Mask<W> MT = mand(M, A1);
+            const int cT = mpopc(MT);
+            const int cF = size - cT;
+            const bool exT = many(mand(MT, A2));
+            const bool exF = many(mand(mandn(M, A1), A2));
+            vote[j] = (cT > n / 2 || exT) ? 1 : ((cF > n / 2 || exF) ? 0 : -1);
+            cd[j] = many(mand(M, A2)) ? 1u : 0u;
+          }
+        } else {  // R1: broadcast vote — BenOr.scala:57-79
+          const int t = mpopc(mand(M, A1));
+          const int f = mpopc(mand(M, A2));
+          if (t > thr) {
+            x[j] = 1;
+            cd[j] = 1;
+          } else if (f > thr) {
+            x[j] = 0;
+            cd[j] = 1;
+          } else if (t > 1) {
+            x[j] = 1;
+          } else if (f > 1) {
+            x[j] = 0;
+          } else {
+            x[j] = sc.coin(k, P.pid(j)) ? 1u : 0u;
+          }
+        }
+        if (halt_round[j] == k) halted[j] = 1;
+      }
+    }
+    check(k + 1, true);
+  }
+  int32_t fx[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) fx[j] = (int32_t)x[j];
+  pk_finish<W>(P, a, i, ck, 5, dec_val, dec_round, halt_round, fx, bc);
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) benor_packed_kernel(KArgs a) {
+  __shared__ BlockCounters bc;
+  counters_init(&bc);
+  __syncthreads();
+  Pk<W> P;
+  P.setup(a.n);
+  InstanceQueue<1> Q;
+  for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
+    const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
+    benor_packed<W>(P, a, i, inst, &bc);
+  }
+  __syncthreads();
+  counters_flush(&bc, a.counters, 5, a.R);
+}
+
 // Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
 // fused Spec module (round_amd/formula.py compile_native(fused=True)).
 template <int W, bool XHO, class SH = NoHook>
@@ -332,6 +496,13 @@ benor_kernel(KArgs a) {
 #ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
+  if constexpr (W > 1) {  // seeded schedule, built-in checker: lane-packed path
+    if (!a.ho_in && !a.trace) {
+      const int pg = pk_grid<PSG_ALG_BENOR, W>((const void*)benor_packed_kernel<W>, a.count);
+      hipLaunchKernelGGL((benor_packed_kernel<W>), dim3(pg), dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
+  }
   if (a.ho_in) hipLaunchKernelGGL((benor_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   else hipLaunchKernelGGL((benor_kernel<W, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();

@@ -774,15 +774,22 @@ struct Sched {
     if (crash_on && valid) {
       const uint64_t w0 = rword(seed, i, ROUND_CRASH, PID_GLOBAL, 0);
       const uint64_t w1 = rword(seed, i, ROUND_CRASH, PID_GLOBAL, 1);
-      const uint32_t f = mulhi32((uint32_t)w0, (uint32_t)args.crash_fmax + 1u);
-      const uint32_t am = (uint32_t)(w0 >> 32) | 1u;
-      const uint32_t off = (uint32_t)w1;
-      const uint32_t n = (uint32_t)args.n;
-      const bool pow2 = (n & (n - 1)) == 0;
-      const uint32_t pos = pow2 ? ((am * (uint32_t)pid + off) & (n - 1)) : (((uint32_t)pid + off % n) % n);
-      if (pos < f)
-        crash_round = (int32_t)mulhi32((uint32_t)rword(seed, i, ROUND_CRASH, (uint32_t)pid, 0), (uint32_t)args.R);
+      crash_round = crash_of(args, i, (uint32_t)pid, w0, w1);
     }
+  }
+
+  // Crash round of process pid (-1 = correct) from the instance's two crash words
+  // w0, w1 (round ROUND_CRASH, pid PID_GLOBAL, words 0 and 1): f = the number of
+  // crashed processes, an affine permutation of the pids picks them.
+  PSG_DEV static int32_t crash_of(const KArgs& args, uint64_t i, uint32_t pid, uint64_t w0, uint64_t w1) {
+    const uint32_t f = mulhi32((uint32_t)w0, (uint32_t)args.crash_fmax + 1u);
+    const uint32_t am = (uint32_t)(w0 >> 32) | 1u;
+    const uint32_t off = (uint32_t)w1;
+    const uint32_t n = (uint32_t)args.n;
+    const bool pow2 = (n & (n - 1)) == 0;
+    const uint32_t pos = pow2 ? ((am * pid + off) & (n - 1)) : ((pid + off % n) % n);
+    if (pos >= f) return -1;
+    return (int32_t)mulhi32((uint32_t)rword(args.seed, i, ROUND_CRASH, pid, 0), (uint32_t)args.R);
   }
 
   PSG_DEV int32_t init_value(int pid, int alg) const {

@@ -9,6 +9,7 @@
 // k = 1 over correct processes and validity (decisions are initial values).
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
+#include "psg_packed.hpp"
 
 namespace psg {
 
@@ -153,6 +154,140 @@ PSG_DEV void floodmin_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashS
   finish_instance<W>(g, a, i, ck, 2, dec_val, dec_round, halt_round, x, bc);
 }
 
+// ---------------------------------------------------------------- crash-stop fast path, lane-packed
+// The same computation as floodmin_fast for n > 64, one wave per instance with the W
+// processes l + 64 j in lane l (psg_packed.hpp): the check's ballots are wave ballots
+// (existential ones of the lane's OR over its slots), the minima are wave reductions
+// of the lane's minimum over its slots, and a round needs no barrier at all. Only the
+// survival words of the crashing senders' 64-pid words are drawn (one Philox call per
+// two words), where the group path draws all W.
+template <int W>
+PSG_DEV void floodmin_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, int32_t* x0lds,
+                             BlockCounters* bc) {
+  const int n = a.n, f = a.param;
+  Sched<W, false> sc;
+  sc.setup(a, inst, P.lane, false);  // uniform parts; crash rounds per slot below
+  int32_t cr[W];
+  pk_crash_rounds<W>(P, a, inst, cr);
+  int32_t x[W], decision[W], dec_val[W], dec_round[W], halt_round[W];
+  uint32_t dec01[W], halt01[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    x[j] = 0;
+    if (P.val[j])
+      x[j] = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + P.pid(j)] : sc.init_value(P.pid(j), PSG_ALG_FLOODMIN);
+    decision[j] = 0;
+    dec_val[j] = 0;
+    dec_round[j] = -1;
+    halt_round[j] = -1;
+    dec01[j] = 0;
+    halt01[j] = 0;
+  }
+  X0Set<W> X0;
+  pk_x0_build<W>(P, X0, x0lds, x);
+  Checks ck;
+  ck.reset();
+  int32_t mU = INT32_MAX;
+  Mask<W> act;
+  // check point c (after round c - 1) and the group minimum over U of round c
+  auto check = [&](int c) {
+    uint32_t anyY = 0, anyBad = 0, undec = 0, alive[W];
+    int32_t mu = INT32_MAX, dmn = INT32_MAX, dmx = INT32_MIN;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const uint32_t crashed = cr[j] >= 0 ? 1u : 0u;
+      alive[j] = P.val[j] & (1u - halt01[j]);
+      const uint32_t inU = alive[j] & (1u - (crashed & (cr[j] <= c ? 1u : 0u)));  // not crashed before or in round c
+      const uint32_t dc = P.val[j] & dec01[j] & (1u - crashed);
+      mu = inU ? min(mu, x[j]) : mu;
+      dmn = dc ? min(dmn, decision[j]) : dmn;
+      dmx = dc ? max(dmx, decision[j]) : dmx;
+      anyY |= dc;
+      anyBad |= P.val[j] & dec01[j] & (1u - X0.contains01(decision[j]));
+      undec |= P.val[j] & (1u - dec01[j]);
+    }
+    act = P.ballot(alive);
+    mU = Grp<1>::dpp_reduce32<false>(mu);
+    dmn = Grp<1>::dpp_reduce32<false>(dmn);
+    dmx = Grp<1>::dpp_reduce32<true>(dmx);
+    const bool one = !pk_any(anyY) || dmn == dmx;  // KAgreement with k = 1 (kagree_check)
+    ck.record(fbit(one, 0) | fbit(!pk_any(anyBad), 1), !pk_any(undec), c, P.lane);
+  };
+  check(0);
+  for (int k = 0; k < a.R; ++k) {
+    if (many(act)) {
+      Mask<W> CN;
+#pragma unroll
+      for (int j = 0; j < W; ++j) CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
+      const Mask<W> CNa = mand(CN, act);
+      int32_t nx[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) nx[j] = min(x[j], mU);
+      // crash round of some alive sender: its message reaches p iff p's survival bit.
+      // Survival word w of p's stream is half w & 1 of Philox call w / 2 (Sched::draw with
+      // drop = 0): the senders are taken by call, two 64-pid words at a time.
+#pragma unroll
+      for (int s = 0; 2 * s < W; ++s) {
+        Mask<W> rem = mzero<W>();
+        rem.w[2 * s] = CNa.w[2 * s];
+        if (2 * s + 1 < W) rem.w[2 * s + 1] = CNa.w[2 * s + 1];
+        if (!many(rem)) continue;
+        uint64_t h0[W], h1[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), (uint32_t)k,
+                                (uint32_t)P.pid(j) + ((uint32_t)s << 16), (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+          h0[j] = (uint64_t)o.x | ((uint64_t)o.y << 32);
+          h1[j] = (uint64_t)o.z | ((uint64_t)o.w << 32);
+        }
+        while (many(rem)) {
+          const int q = mtake_first(rem);
+          const int32_t xq = P.bcast(x, q);
+          const bool hi = (q >> 6) & 1;
+          const int qb = q & 63;
+#pragma unroll
+          for (int j = 0; j < W; ++j)
+            if (((hi ? h1[j] : h0[j]) >> qb) & 1ull) nx[j] = min(nx[j], xq);
+        }
+      }
+      const bool decideNow = a.variant == 1 ? (k >= f - 1) : (k > f);  // FloodMin.scala:27 (variant 1: mutation)
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        if (halt01[j]) continue;
+        x[j] = nx[j];
+        if (decideNow) {
+          dec_val[j] = x[j];
+          dec_round[j] = k;
+          dec01[j] = 1;
+          decision[j] = x[j];
+          halt_round[j] = k;
+          halt01[j] = 1;
+        }
+      }
+    }
+    check(k + 1);
+  }
+  pk_finish<W>(P, a, i, ck, 2, dec_val, dec_round, halt_round, x, bc);
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) floodmin_packed_kernel(KArgs a) {
+  __shared__ BlockCounters bc;
+  __shared__ int32_t x0tab[4][X0Set<W>::kSlots];
+  counters_init(&bc);
+  __syncthreads();
+  Pk<W> P;
+  P.setup(a.n);
+  int32_t* x0lds = x0tab[threadIdx.x >> 6];
+  InstanceQueue<1> Q;
+  for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
+    const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
+    floodmin_packed<W>(P, a, i, inst, x0lds, &bc);
+  }
+  __syncthreads();
+  counters_flush(&bc, a.counters, 2, a.R);
+}
+
 // Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
 // fused Spec module (round_amd/formula.py compile_native(fused=True)).
 template <int W, bool XHO, class SH = NoHook>
@@ -294,6 +429,13 @@ floodmin_kernel(KArgs a) {
 #ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
+  if constexpr (W > 1) {  // seeded crash-stop schedule, built-in checker: lane-packed fast path
+    if (!a.ho_in && !a.trace && a.drop_log2 == 0 && a.good_p32 == 0 && a.ho_min < 0) {
+      const int pg = pk_grid<PSG_ALG_FLOODMIN, W>((const void*)floodmin_packed_kernel<W>, a.count);
+      hipLaunchKernelGGL((floodmin_packed_kernel<W>), dim3(pg), dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
+  }
   if (a.ho_in) hipLaunchKernelGGL((floodmin_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   else hipLaunchKernelGGL((floodmin_kernel<W, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();

@@ -37,6 +37,13 @@ CASES = [
     ("fm-n64-f8", psync.FloodMin(8), 64, 1000, dict(seed=18)),
     ("fm-mutant-n16", psync.FloodMin(3, variant=1), 16, 2000, dict(seed=19)),
     ("fm-n256-loss", psync.FloodMin(2), 256, 100, dict(seed=20, schedule=H(drop_log2=2, crash_fmax=2))),
+    # lane-packed crash-stop path (n > 64, seeded crash-only schedules): ragged n, every W
+    ("fm-n65-f3", psync.FloodMin(3), 65, 400, dict(seed=60)),
+    ("fm-n128-f0", psync.FloodMin(0), 128, 300, dict(seed=61)),
+    ("fm-n130-mutant", psync.FloodMin(6, variant=1), 130, 300, dict(seed=62, value_range=5)),
+    ("fm-n200-f16", psync.FloodMin(16), 200, 200, dict(seed=63, value_range=40)),
+    ("fm-n256-f64", psync.FloodMin(64), 256, 60, dict(seed=64)),
+    ("fm-n256-f8-V3", psync.FloodMin(8), 256, 300, dict(seed=65, value_range=3)),
     ("kset-n256-k2", psync.KSetAgreement(2), 256, 24, dict(seed=21)),
     ("kset-n64-k3-crash", psync.KSetAgreement(3), 64, 400, dict(seed=22, schedule=H(drop_log2=0, crash_fmax=10,
                                                                                        good_round=0.0))),
@@ -119,6 +126,21 @@ def test_host_supplied_inputs(oracle_mod):
         gr.load_inputs(50, count, init)
         res = gr.run(50, count, per_instance=True)
     osum, opi, _ = oracle_mod.run(gr.cfg, 50, count, init=init, per_instance=True)
+    _cmp_summary(res.summary, osum, gr.cfg.rounds)
+    assert [_inst_tuple(s) for s in res.per_instance] == [_inst_tuple(s) for s in opi]
+
+
+@pytest.mark.parametrize("alg,n", [(psync.FloodMin(5), 256), (psync.FloodMin(3), 100), (psync.BenOr(), 128)],
+                         ids=["fm-n256", "fm-n100", "benor-n128"])
+def test_host_supplied_inputs_wide(alg, n, oracle_mod):
+    """Caller-provided initial values on the wide fast paths (lane-packed kernels)."""
+    count = 150
+    vr = 2 if isinstance(alg, psync.BenOr) else 1000
+    init = [[(i * 7 + p * 13) % vr + (0 if vr == 2 else -500) for p in range(n)] for i in range(count)]
+    with psync.GpuRound(alg, n, seed=32, batch_capacity=count) as gr:
+        gr.load_inputs(70, count, init)
+        res = gr.run(70, count, per_instance=True)
+    osum, opi, _ = oracle_mod.run(gr.cfg, 70, count, init=init, per_instance=True)
     _cmp_summary(res.summary, osum, gr.cfg.rounds)
     assert [_inst_tuple(s) for s in res.per_instance] == [_inst_tuple(s) for s in opi]
 
