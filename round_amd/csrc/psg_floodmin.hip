@@ -271,7 +271,7 @@ PSG_DEV void floodmin_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_
 }
 
 template <int W>
-__global__ void __launch_bounds__(256) floodmin_packed_kernel(KArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_PK_WPE))) floodmin_packed_kernel(KArgs a) {
   __shared__ BlockCounters bc;
   __shared__ int32_t x0tab[4][X0Set<W>::kSlots];
   counters_init(&bc);

@@ -11,6 +11,11 @@
 #pragma once
 #include "psg_device.hpp"
 
+#ifndef PSG_PK_WPE
+#define PSG_PK_WPE 5  // waves/SIMD the packed kernels are register-allocated for: 4 -> 5 measured
+                      // +6 % (FloodMin C4 f=8 6.60 -> 6.26 ms) and +7 % (BenOr C5 42.6 -> 39.8 ms)
+#endif
+
 namespace psg {
 
 template <int W>

@@ -54,6 +54,15 @@ CASES = [
     ("benor-n4", psync.BenOr(), 4, 3000, dict(seed=26)),
     ("benor-n64-mutant", psync.BenOr(variant=1), 64, 500, dict(seed=27)),
     ("benor-n200-W4", psync.BenOr(), 200, 60, dict(seed=28, rounds=20)),
+    # lane-packed built-in-checker path (n > 64, seeded schedules): ragged n, every W, every schedule family
+    ("benor-n65", psync.BenOr(), 65, 400, dict(seed=66)),
+    ("benor-n128-R64", psync.BenOr(), 128, 200, dict(seed=67, rounds=64)),
+    ("benor-n100-crash-good", psync.BenOr(), 100, 300, dict(seed=68, schedule=H(drop_log2=1, good_round=0.3,
+                                                                                 crash_fmax=30))),
+    ("benor-n150-pureho", psync.BenOr(), 150, 200, dict(seed=69, schedule=H(drop_log2=2, good_round=0.0,
+                                                                           self_bit=False))),
+    ("benor-n192-mutant", psync.BenOr(variant=1), 192, 150, dict(seed=70)),
+    ("benor-n256-W4", psync.BenOr(), 256, 80, dict(seed=71, rounds=24)),
     # second wave
     ("otr2-n64-V4", psync.OTR2(), 64, 2000, dict(value_range=4, seed=40)),
     ("otr2-mutant-n8", psync.OTR2(variant=1), 8, 3000, dict(schedule=H(drop_log2=1, good_round=0.0), seed=41)),
