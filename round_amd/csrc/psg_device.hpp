@@ -1260,11 +1260,32 @@ struct X0Set {
   }
 };
 
-// Candidate for a strict-majority value among the valid lanes of the group
-// (Boyer-Moore pair cancellation as a butterfly reduction): if some value
-// occurs more than n/2 times, it is returned; otherwise an arbitrary value.
+#ifndef PSG_MAJ_BITVOTE
+#define PSG_MAJ_BITVOTE 8  // W == 1: bitwise vote when at most this many bits differ (0: off)
+#endif
+// Candidate for a strict-majority value among the valid lanes of the group: if some
+// value occurs more than n/2 times, it is returned; otherwise an arbitrary value.
+// W == 1, few differing bits: a bitwise vote. A value held by more than half of the
+// lanes agrees with more than half of them on every bit, so its bit b is the majority
+// bit b (popcount of a ballot); bits on which every lane agrees come from the AND.
+// Otherwise Boyer-Moore pair cancellation as a butterfly reduction (ds_bpermute steps).
 template <int W>
 PSG_DEV int32_t majority_candidate(Grp<W>& g, int32_t x) {
+  if constexpr (W == 1 && PSG_MAJ_BITVOTE > 0) {
+    const uint32_t u = (uint32_t)x;
+    const uint32_t any1 = wave_or(g.valid ? u : 0u), any0 = wave_or(g.valid ? ~u : 0u);
+    uint32_t diff = any1 & any0;  // bits set in some lane and clear in another
+    if (__builtin_popcount(diff) <= PSG_MAJ_BITVOTE) {
+      const int half = __popcll(g.vmask) / 2;
+      uint32_t m = any1 & ~any0;  // bits set in every lane
+      while (diff) {
+        const int b = __builtin_ctz(diff);
+        diff &= diff - 1u;
+        if (__popcll(__builtin_amdgcn_ballot_w64((u >> b) & 1u) & g.vmask) > half) m |= 1u << b;
+      }
+      return (int32_t)m;
+    }
+  }
   int32_t c = x;
   int32_t k = g.valid ? 1 : 0;
 #pragma unroll

@@ -309,6 +309,30 @@ PSG_DEV int32_t exists_int_guard(Ctx<W>& x, int32_t t, const int32_t* staged, in
   return acc;
 }
 
+// V.exists(v => ... && P.forall(i => ... && (cond(i) ==> term(i) == v) && ...) && ...): once
+// some process has an active pin (cond true), a witness must equal that process's term, so
+// the body is evaluated at that one value (the first pinned process, its first active pin);
+// with no pin active, `general` (the finitization) decides it. `act` / `val`: the lane's
+// process's pin flag and pinned value.
+template <int W, class FA, class FV, class Fn, class Gen>
+PSG_DEV int32_t exists_int_pin(Ctx<W>& x, FA act, FV val, int32_t* scratch, Fn fn, Gen general) {
+  const int32_t mine = val(x.g.pid);
+  const Mask<W> m = x.g.ballot(act(x.g.pid) != 0);
+  if (many(m)) {
+    int32_t v;
+    if constexpr (W == 1) {
+      v = readlane32(mine, mfirst(m));
+    } else {
+      scratch[x.g.pid] = mine;
+      __syncthreads();
+      v = rfl32(scratch[mfirst(m)]);
+      __syncthreads();
+    }
+    return fn(v) != 0 ? 1 : 0;
+  }
+  return general();
+}
+
 // ---------------------------------------------------------------- arithmetic with Scala Int semantics
 PSG_DEV int32_t idiv(int32_t a, int32_t b) { return b == 0 ? 0 : (a == INT32_MIN && b == -1) ? a : a / b; }
 PSG_DEV int32_t imod(int32_t a, int32_t b) { return (b == 0 || b == -1) ? 0 : a % b; }

@@ -771,7 +771,10 @@ class _Gen:
         if isinstance(e, Contains):
             val, lane = self.gen(e.e, in_lane, vi_depth)
             v = f"b{next(self.k)}"
-            self.names[e.comp.var.uid] = (v, lane, False)
+            own = isinstance(e.e, Var) and self.names.get(e.e.uid, (None, False, False))[2]
+            # A.contains(i) for the lane's own process i: the comprehension's variable is that
+            # process too (its fields are the lane's registers, not a gather)
+            self.names[e.comp.var.uid] = (val, True, True) if own else (v, lane, False)
             body, lb = self.gen(e.comp.body, in_lane, vi_depth)
             return f"([&](int32_t {v}) -> int32_t {{ return {body}; }})({val})", lane or lb
         if isinstance(e, Quant):
@@ -820,6 +823,34 @@ class _Gen:
         if q.kind == "vbool":
             body, lane = self.gen(q.body, in_lane, vi_depth)
             return f"spec::exists_bool<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", lane
+        pins = None if in_lane else _pins(q.body, q.var.uid)
+        if pins is not None:
+            # equality pins: a conjunct P.forall(i => ... && (cond(i) ==> term(i) == v) && ...)
+            # leaves v = term(i) as the only candidate once some process has cond(i); with
+            # none active, the finitization below decides it
+            fq, plist = pins
+            pl = f"p{next(self.k)}"
+            self.names[fq.var.uid] = (pl, True, True)
+            conds, vals = [], []
+            for cond, term in plist:
+                conds.append("1" if cond is None else f"(int32_t)(({self.gen(cond, True, vi_depth)[0]}) != 0)")
+                vals.append(self.gen(term, True, vi_depth)[0])
+            act = " | ".join(conds)
+            val = vals[-1]
+            for cc, tc in reversed(list(zip(conds[:-1], vals[:-1]))):
+                val = f"(({cc}) != 0 ? ({tc}) : ({val}))"
+            general, _ = self._vint_unpinned(q, v, in_lane, vi_depth)
+            self.names[q.var.uid] = (v, False, False)
+            body, _ = self.gen(q.body, in_lane, vi_depth + 1)
+            self.max_vi = max(self.max_vi, vi_depth + 1)
+            return (f"spec::exists_int_pin<W>(x, [&](int32_t {pl}) -> int32_t {{ return {act}; }}, "
+                    f"[&](int32_t {pl}) -> int32_t {{ return {val}; }}, scratch + {vi_depth} * 64 * W, "
+                    f"[&](int32_t {v}) -> int32_t {{ return {body}; }}, [&]() -> int32_t {{ return {general}; }})"), True
+        return self._vint_unpinned(q, v, in_lane, vi_depth)
+
+    def _vint_unpinned(self, q, v, in_lane, vi_depth):
+        """V.exists over Int: count-guarded candidates, else the general finitization."""
+        self.names[q.var.uid] = (v, False, False)
         guard = _count_guard(q)
         if guard is not None:
             # a conjunct P.filter(i => i.f == v).size >= L restricts the witnesses to values
@@ -917,6 +948,80 @@ def _eq_only(q) -> bool:
     return True
 
 
+def _pins(body, uid):
+    """Equality pins of the V.exists variable `uid` in `body`: the first top-level conjunct
+    P.forall(i => c1 && c2 && ...) having conjuncts `cond ==> term == v` or `term == v`
+    (cond, term free of v): (that forall, [(cond or None, term)]), else None."""
+    for c in _conjuncts(body):
+        if not (isinstance(c, Quant) and c.kind == "forall"):
+            continue
+        out = []
+        for d in _conjuncts(c.body):
+            cond, eq = (d.x, d.y) if isinstance(d, Bin) and d.op == "IMPL" else (None, d)
+            if cond is not None and uid in _free_vars(cond):
+                continue
+            if not (isinstance(eq, Bin) and eq.op == "EQ"):
+                continue
+            for term, other in ((eq.x, eq.y), (eq.y, eq.x)):
+                if isinstance(other, Var) and other.uid == uid and uid not in _free_vars(term):
+                    out.append((cond, term))
+                    break
+        if out:
+            return c, out
+    return None
+
+
+# The swap below is exact but measured slower on LastVoting's majority clause (fused LV
+# n=64: 205 -> 346 ms per 1.25e7 instances, scripts/fused_breakdown.py): the original order
+# finds its witness early (the first value candidate with the first passing round), the
+# swapped one tries every round candidate. Off by default; the tests exercise both.
+SWAP_VINT = False
+
+
+def _rewrite_vint(e, memo=None):
+    """Rewrites of V.exists over Int for the native lowering, exact for every input (the
+    domain is non-empty and both sides are decided exactly):
+      V.exists(v => V.exists(t => B)) -> V.exists(t => V.exists(v => B)) when v has equality
+        pins in B and t has none (the pinned variable innermost, where one candidate decides it);
+      V.exists(v => A && B(v)) -> A && V.exists(v => B(v)) for the conjuncts A free of v.
+    Shared subformulas stay shared (memo by object)."""
+    memo = {} if memo is None else memo
+    k = id(e)
+    if k in memo and memo[k][0] is e:  # the key object is kept alive with its entry (ids are reused)
+        return memo[k][1]
+    out = e
+    if (SWAP_VINT and isinstance(e, Quant) and e.kind == "vint" and isinstance(e.body, Quant)
+            and e.body.kind == "vint"
+            and _pins(e.body.body, e.var.uid) is not None and _pins(e.body.body, e.body.var.uid) is None):
+        out = _rewrite_vint(Quant("vint", e.body.var, Quant("vint", e.var, e.body.body)), memo)
+    elif isinstance(e, Quant):
+        b = _rewrite_vint(e.body, memo)
+        out = e if b is e.body else Quant(e.kind, e.var, b)
+        if out.kind == "vint":
+            out = _vint_step(out, memo)
+    elif isinstance(e, Bin):
+        x, y = _rewrite_vint(e.x, memo), _rewrite_vint(e.y, memo)
+        out = e if (x is e.x and y is e.y) else Bin(e.op, x, y)
+    elif isinstance(e, Un):
+        x = _rewrite_vint(e.x, memo)
+        out = e if x is e.x else Un(e.op, x)
+    elif isinstance(e, Contains):
+        b, x = _rewrite_vint(e.comp.body, memo), _rewrite_vint(e.e, memo)
+        out = e if (b is e.comp.body and x is e.e) else Contains(Comprehension(e.comp.var, b), x)
+    memo[k] = (e, out)
+    return out
+
+
+def _vint_step(q, memo):
+    v, body = q.var.uid, q.body
+    cs = _conjuncts(body)
+    free = [c for c in cs if v not in _free_vars(c)]
+    bound = [c for c in cs if v in _free_vars(c)]
+    if free and bound:
+        return And(*free, Quant("vint", q.var, And(*bound)))
+    return q
+
+
 def _count_guard(q):
     """A top-level conjunct `P.filter(i => i.f == v).size OP thr` (OP in >, >=, ==; thr
     free of bound variables) of V.exists(v => body): ((f, tag), thr, OP) or None."""
@@ -947,14 +1052,17 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
     prog = compile_spec(spec, alg)
     gen = _Gen(ALG_FIELDS.get(alg) if alg is not None else None)
     guard = _rinv_guard(spec)
-    invs = [inv if guard is None else (inv & guard) for inv in spec.invariants]
+    memo = {}
+    invs = [_rewrite_vint(inv if guard is None else (inv & guard), memo) for inv in spec.invariants]
+    props = [(name, _rewrite_vint(f, memo)) for name, f in spec.properties]
+    safety = None if spec.safety_predicate is None else _rewrite_vint(spec.safety_predicate, memo)
     lines = []
     slot = 0
     # common closed subformulas (the same Formula object used by several slots, e.g.
     # OTR's keepInit in Invariant0 and Invariant1): hoisted, evaluated once per check point
-    roots = list(invs) + [f for name, f in spec.properties if name != "Termination"]
-    if spec.safety_predicate is not None:
-        roots.append(spec.safety_predicate)
+    roots = list(invs) + [f for name, f in props if name != "Termination"]
+    if safety is not None:
+        roots.append(safety)
     seen, order = {}, []
 
     def visit(e):
@@ -983,15 +1091,15 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
             lines.append(f"    if (inv{k} == 0) fb |= 1u << {slot};")
             slot += 1
     term = None
-    for name, f in spec.properties:
+    for name, f in props:
         if name == "Termination":
             term, _ = gen.gen(f, False, 0)
             continue
         c, _ = gen.gen(f, False, 0)
         lines.append(f"    if (({c}) == 0) fb |= 1u << {slot};  // {name}")
         slot += 1
-    if spec.safety_predicate is not None:
-        c, _ = gen.gen(spec.safety_predicate, False, 0)
+    if safety is not None:
+        c, _ = gen.gen(safety, False, 0)
         lines.append(f"    if (({c}) == 0) fb |= 1u << {slot};  // SafetyPredicate")
         slot += 1
     assert slot == len(prog.slot_entry)

@@ -80,6 +80,26 @@ def set_operations():
     ])
 
 
+def pin_shapes():
+    """V.exists shapes with equality pins (a P.forall conjunct `cond ==> term == v` leaves one
+    candidate once some process has cond): conditional and unconditional pins, several pins,
+    v-free conjuncts hoisted out, two nested V.exists swapped so the pinned one is innermost
+    (LastVoting's majority shape), both nested variables pinned, pins on old state."""
+    return F.Spec(properties=[
+        ("PinSwap", V.exists(lambda v: V.exists(lambda t: (P.filter(lambda i: i.x >= t).size > n // 2)
+                                                 & P.forall(lambda i: (i.x >= t).implies(i.x == v)
+                                                            & i.decided.implies(i.decision == v))))),
+        ("PinPlain", V.exists(lambda v: P.forall(lambda i: i.x == v))),
+        ("PinTwo", V.exists(lambda v: P.forall(lambda i: i.decided.implies(i.decision == v)
+                                               & (i.x > 2).implies(i.x == v)) & (v > 0))),
+        ("PinHoist", V.exists(lambda v: (r > 1) & P.forall(lambda i: i.decided.implies(i.decision == v))
+                              & (P.filter(lambda i: i.x == v).size >= 1))),
+        ("PinNested", V.exists(lambda v: V.exists(lambda w: P.forall(lambda i: i.decided.implies(i.decision == v))
+                                                  & P.forall(lambda j: (j.x > v).implies(j.x == w))))),
+        ("PinOld", V.exists(lambda v: P.forall(lambda i: old(i.decided).implies(old(i.decision) == v)))),
+    ])
+
+
 # (id, algorithm, n, make_config kwargs, spec factory)
 CUSTOM = [
     ("fm-n12", psync.FloodMin(2), 12, dict(value_range=8, schedule=H(drop_log2=0, good_round=0.0, crash_fmax=3)),
@@ -101,4 +121,9 @@ CUSTOM = [
                                                                             crash_fmax=3)), set_operations),
     ("fm-n8-shapes", psync.FloodMin(2), 8, dict(value_range=3, schedule=H(drop_log2=0, good_round=0.0,
                                                                            crash_fmax=3)), witness_shapes),
+    ("otr-n16-pins", psync.OTR(), 16, dict(value_range=3), pin_shapes),
+    ("otr2-n100-pins", psync.OTR2(), 100, dict(value_range=4), pin_shapes),
+    ("fm-n8-pins", psync.FloodMin(2), 8, dict(value_range=3, schedule=H(drop_log2=0, good_round=0.0,
+                                                                         crash_fmax=3)), pin_shapes),
+    ("lv-n8-pins", psync.LastVoting(), 8, dict(value_range=3), pin_shapes),
 ]

@@ -53,6 +53,59 @@ def test_custom_specs_match_direct_evaluation(cid, alg, n, kw, mk, oracle_mod):
     assert ff == rf and tm == rt
 
 
+def _rewritten(spec):
+    """The Spec with every formula passed through the native lowering's V.exists rewrites."""
+    memo = {}
+    g = F._rinv_guard(spec)
+    invs = [F._rewrite_vint(inv if g is None else (inv & g), memo) for inv in spec.invariants]
+    props = [(name, F._rewrite_vint(f, memo)) for name, f in spec.properties]
+    sp = None if spec.safety_predicate is None else F._rewrite_vint(spec.safety_predicate, memo)
+    plain = [inv if g is None else (inv & g) for inv in spec.invariants]
+    return (F.Spec(plain, [], spec.properties, spec.safety_predicate, phase_length=spec.phase_length),
+            F.Spec(invs, [], props, sp, phase_length=spec.phase_length))
+
+
+REWRITE_CASES = [(f"ref-{a}", alg, n, kw, F.REFERENCE_SPECS[a]) for a, alg, n, kw in [
+    (abi.PSG_ALG_OTR, psync.OTR(), 16, dict(value_range=3, schedule=H(drop_log2=1))),
+    (abi.PSG_ALG_OTR2, psync.OTR2(), 10, {}),
+    (abi.PSG_ALG_LAST_VOTING, psync.LastVoting(), 16, dict(value_range=3, schedule=H(
+        drop_log2=1, good_round=0.0, crash_fmax=7))),
+    (abi.PSG_ALG_LAST_VOTING, psync.LastVoting(variant=1), 6, dict(value_range=5)),
+    (abi.PSG_ALG_BENOR, psync.BenOr(), 8, {})]] + [c for c in spec_cases.CUSTOM if c[2] <= 16]
+
+
+@pytest.mark.parametrize("swap", [False, True], ids=["hoist", "swap+hoist"])
+@pytest.mark.parametrize("cid,alg,n,kw,mk", REWRITE_CASES, ids=[c[0] for c in REWRITE_CASES])
+def test_native_rewrites_are_exact(cid, alg, n, kw, mk, oracle_mod, swap, monkeypatch):
+    """The V.exists rewrites of the native lowering (swap to put the pinned variable
+    innermost, hoist conjuncts free of the variable) give the same results as the
+    Spec as written, under the CPU interpreter, check point by check point."""
+    monkeypatch.setattr(F, "SWAP_VINT", swap)
+    cfg = psync.make_config(alg, n, seed=29, **kw)
+    orig, rw = _rewritten(mk())
+    cnt = 300
+    tr = oracle_mod.trace(cfg, 0, cnt)
+    f1, t1 = oracle_mod.vm_run(F.compile_spec(orig, alg.alg_id), tr, cnt, n, cfg.rounds)
+    f2, t2 = oracle_mod.vm_run(F.compile_spec(rw, alg.alg_id), tr, cnt, n, cfg.rounds)
+    assert f1 == f2 and t1 == t2
+
+
+def test_rewrites_shapes():
+    """LastVoting's majority clause: the pinned value variable moves innermost and the
+    conjuncts free of it are hoisted out (the lowering then takes one candidate)."""
+    spec = F.lv_spec()
+    F.SWAP_VINT = True
+    try:
+        mb = F._rewrite_vint(spec.invariants[0])
+    finally:
+        F.SWAP_VINT = False
+    vints = [x for x in F._walk(mb) if isinstance(x, F.Quant) and x.kind == "vint"]
+    assert len(vints) == 2
+    outer, inner = vints
+    assert F._pins(inner.body, inner.var.uid) is not None  # v, pinned by x / decision / vote
+    assert F._pins(outer.body, outer.var.uid) is None       # t
+
+
 def test_custom_specs_find_violations(oracle_mod):
     """A false property is reported at the first check point it fails."""
     spec = F.Spec(properties=[("NobodyDecides", F.P.forall(lambda i: ~i.decided))])
