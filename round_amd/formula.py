@@ -948,22 +948,30 @@ def _eq_only(q) -> bool:
     return True
 
 
-def _pins(body, uid):
+def _pins(body, uid, banned=frozenset()):
     """Equality pins of the V.exists variable `uid` in `body`: the first top-level conjunct
     P.forall(i => c1 && c2 && ...) having conjuncts `cond ==> term == v` or `term == v`
-    (cond, term free of v): (that forall, [(cond or None, term)]), else None."""
+    (cond, term free of v): (that forall, [(cond or None, term)]), else None. A conjunct
+    V.exists(t => B) is searched too, for pins free of t: they constrain v for every t, so
+    they pin v across the inner quantifier (LastVoting: decided ==> decision == v)."""
     for c in _conjuncts(body):
+        if isinstance(c, Quant) and c.kind == "vint":
+            got = _pins(c.body, uid, banned | {c.var.uid})
+            if got is not None:
+                return got
+            continue
         if not (isinstance(c, Quant) and c.kind == "forall"):
             continue
         out = []
         for d in _conjuncts(c.body):
             cond, eq = (d.x, d.y) if isinstance(d, Bin) and d.op == "IMPL" else (None, d)
-            if cond is not None and uid in _free_vars(cond):
+            if cond is not None and (uid in _free_vars(cond) or _free_vars(cond) & banned):
                 continue
             if not (isinstance(eq, Bin) and eq.op == "EQ"):
                 continue
             for term, other in ((eq.x, eq.y), (eq.y, eq.x)):
-                if isinstance(other, Var) and other.uid == uid and uid not in _free_vars(term):
+                if (isinstance(other, Var) and other.uid == uid and uid not in _free_vars(term)
+                        and not (_free_vars(term) & banned)):
                     out.append((cond, term))
                     break
         if out:
