@@ -10,6 +10,7 @@
 // message in Scala Map iteration order (CHAMP for > 4 entries).
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
+#include "psg_packed.hpp"
 
 namespace psg {
 
@@ -46,6 +47,265 @@ PSG_DEV Mask<W> load_t(const uint64_t* ts, int q) {
 #pragma unroll
   for (int w = 0; w < W; ++w) m.w[w] = ts[q * W + w];
   return m;
+}
+
+// `content.find(_._1)` of receiver p (KSetAgreement.scala:53): the first decider message in
+// Scala Map iteration order — the first pid of cand up to 4 mailbox entries (Map1..Map4)
+// or when the candidates agree on t; otherwise the CHAMP order's first (min sort key).
+template <int W>
+PSG_DEV int kset_find(const KArgs& a, const uint64_t* ts, const Mask<W>& M, const Mask<W>& cand) {
+  int qs = mfirst(cand);
+  if (a.tiebreak == PSG_TIE_CHAMP && mpopc(M) > 4 && mpopc(cand) > 1) {
+    const Mask<W> t0 = load_t<W>(ts, qs);
+    bool differ = false;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint64_t m = cand.w[w];
+      while (m) {
+        const int q = w * 64 + __builtin_ctzll(m);
+        m &= m - 1;
+        if (!meq(load_t<W>(ts, q), t0)) differ = true;
+      }
+    }
+    if (differ) {
+      uint64_t best = ~0ull;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        uint64_t m = cand.w[w];
+        while (m) {
+          const int q = w * 64 + __builtin_ctzll(m);
+          m &= m - 1;
+          const uint32_t hq = scala_improve((uint32_t)q);
+          int depth = 0;
+#pragma unroll
+          for (int v = 0; v < W; ++v) {
+            uint64_t mm = M.w[v];
+            while (mm) {
+              const int f = v * 64 + __builtin_ctzll(mm);
+              mm &= mm - 1;
+              if (f != q) depth = max(depth, champ_cpl(hq, scala_improve((uint32_t)f)));
+            }
+          }
+          const uint64_t key = champ_key(hq, depth);
+          if (key < best) {
+            best = key;
+            qs = q;
+          }
+        }
+      }
+    }
+  }
+  return qs;
+}
+
+// ---------------------------------------------------------------- lane-packed path (n > 64)
+// kset_body's built-in-checker path with one wave per instance and the W processes
+// l + 64 j in lane l (psg_packed.hpp): the t masks are staged in this wave's LDS (one
+// 8 W-byte row per process) for the uniform class reads and the per-lane find; the
+// k-agreement check's ballots are wave ballots; no round needs a block barrier.
+template <int W>
+struct KsPk {
+  uint64_t ts[64 * W * W];
+  int32_t x0s[64 * W];
+};
+
+template <int W>
+PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, KsPk<W>& L, int32_t* x0lds,
+                         BlockCounters* bc) {
+  const int n = a.n, kk = a.param;
+  const int need = a.variant == 1 ? 1 : n - kk;  // same.size > n - k (KSetAgreement.scala:56)
+  Sched<W, false> sc;
+  sc.setup(a, inst, P.lane, false);
+  sc.prep_good(0, P.lane, a.R);
+  int32_t cr[W];
+  pk_crash_rounds<W>(P, a, inst, cr);
+  int32_t x0[W], decision[W], dec_val[W], dec_round[W], halt_round[W];
+  uint32_t decider[W], decided[W], halted[W];
+  Mask<W> t[W];
+  int32_t xmin_l = INT32_MAX;
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    x0[j] = 0;
+    if (P.val[j])
+      x0[j] = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + P.pid(j)] : sc.init_value(P.pid(j), PSG_ALG_KSET);
+    L.x0s[P.pid(j)] = x0[j];
+    if (P.val[j]) xmin_l = min(xmin_l, x0[j]);
+    // t = Map(id -> io.initialValue); decider = false (KSetAgreement.scala:27-31)
+    t[j] = mzero<W>();
+    if (P.val[j]) t[j].w[j] = 1ull << P.lane;
+    decision[j] = dec_val[j] = 0;
+    dec_round[j] = halt_round[j] = -1;
+    decider[j] = decided[j] = halted[j] = 0;
+  }
+  X0Set<W> X0;
+  pk_x0_build<W>(P, X0, x0lds, x0);  // ends with an LDS fence: x0s visible too
+  const int32_t xmin = Grp<1>::dpp_reduce32<false>(xmin_l);
+  uint32_t emin[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) emin[j] = P.val[j] & eq01(x0[j], xmin);
+  const Mask<W> Emin = P.ballot(emin);
+  Checks ck;
+  ck.reset();
+  // k-agreement (kagree_check): decisions of never-crashed deciders number <= k; every
+  // decision is an initial value
+  auto check = [&](int c) {
+    uint32_t dc[W], undec = 0, bad = 0;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      dc[j] = P.val[j] & decided[j] & (cr[j] >= 0 ? 0u : 1u);
+      undec |= P.val[j] & (1u - decided[j]);
+      bad |= P.val[j] & decided[j] & (1u - X0.contains01(decision[j]));
+    }
+    Mask<W> Y = P.ballot(dc);
+    int distinct = 0;
+    while (many(Y) && distinct <= kk) {
+      const int32_t dv = P.bcast(decision, mfirst(Y));
+      uint32_t eq[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) eq[j] = dc[j] & eq01(decision[j], dv);
+      Y = mandn(Y, P.ballot(eq));
+      ++distinct;
+    }
+    ck.record(fbit(distinct <= kk, 0) | fbit(!pk_any(bad), 1), !pk_any(undec), c, P.lane);
+  };
+  check(0);
+  Mask<W> act;
+  {
+    uint32_t al[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) al[j] = P.val[j];
+    act = P.ballot(al);
+  }
+  for (int k = 0; k < a.R; ++k) {
+    if (many(act)) {
+      Mask<W> goodS;
+      const bool good = sc.good_round(k, P.lane, a.R, goodS);
+      Mask<W> CB = mzero<W>(), CN = mzero<W>();
+      if (sc.crash_on) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          CB.w[j] = __builtin_amdgcn_ballot_w64(cr[j] >= 0 && cr[j] < k);
+          CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
+        }
+      }
+      const Mask<W> Dm = mand(P.ballot(decider), act);  // senders' decider flags (pre-state)
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+#pragma unroll
+        for (int w = 0; w < W; ++w) L.ts[P.pid(j) * W + w] = t[j].w[w];
+      lds_sync<1>();
+      // round 0 (every alive sender still holds only its own origin): closed form below
+      uint32_t notown[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        Mask<W> own = mzero<W>();
+        if (P.val[j]) own.w[j] = 1ull << P.lane;
+        notown[j] = meq(t[j], own) ? 0u : 1u;
+      }
+      const bool closed = !many(mand(act, P.ballot(notown)));
+      // one slot at a time (its HO set M, its merge or adoption); the t registers keep the
+      // pre-round state until every slot is done (the class ballots read every slot's t)
+      Mask<W> tnew[W];
+      uint32_t becomeDec[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        tnew[j] = t[j];
+        becomeDec[j] = 0;
+        const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
+        const uint32_t live = P.val[j] & (1u - halted[j]) & (1u - decider[j]);
+        const uint32_t hc = many(mand(M, Dm)) ? 1u : 0u;
+        const uint32_t adopt = live & hc, mergep = live & (1u - hc);
+        if (pk_any(mergep)) {
+          // same = mailbox.filter(_._2._2 == t).size; uni = t ++ every received t, by classes
+          // of equal t among the alive senders (kset_body)
+          constexpr int kClasses = 8;
+          int same = 0;
+          Mask<W> uni = t[j];
+          Mask<W> rem = act;
+          if (closed) {
+            same = ((M.w[j] >> P.lane) & 1ull) ? 1 : 0;
+            uni = mor(t[j], M);
+            rem = mzero<W>();
+          }
+          for (int cls = 0; cls < kClasses && many(rem); ++cls) {
+            const Mask<W> tq = load_t<W>(L.ts, mfirst(rem));
+            uint32_t mine[W];
+#pragma unroll
+            for (int jj = 0; jj < W; ++jj) mine[jj] = meq(t[jj], tq) ? 1u : 0u;
+            const Mask<W> E = mand(P.ballot(mine), rem);
+            rem = mandn(rem, E);
+            const Mask<W> ME = mand(M, E);
+            if (mine[j]) same = mpopc(ME);
+            if (many(ME)) uni = mor(uni, tq);
+          }
+          while (many(rem)) {
+            const int q = mtake_first(rem);
+            const Mask<W> tq = load_t<W>(L.ts, q);
+            if (mtest(M, q)) {
+              same += meq(tq, t[j]) ? 1 : 0;
+              uni = mor(uni, tq);
+            }
+          }
+          if (mergep) {
+            if (same > need) becomeDec[j] = 1;
+            else tnew[j] = uni;
+          }
+        }
+        if (adopt) {  // t = content.find(_._1).get._2 — first decider message in iteration order
+          tnew[j] = load_t<W>(L.ts, kset_find<W>(a, L.ts, M, mand(M, Dm)));
+          becomeDec[j] = 1;
+        }
+        if (!halted[j] && decider[j]) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:48-50)
+          const int32_t v = kset_pick<W>(t[j], L.x0s, Emin, xmin);
+          dec_val[j] = v;
+          dec_round[j] = k;
+          decided[j] = 1;
+          decision[j] = v;
+          halt_round[j] = k;
+        }
+      }
+      lds_sync<1>();  // all reads of ts done before the next round restages it
+      uint32_t al[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        if (!halted[j]) {
+          t[j] = tnew[j];
+          decider[j] |= becomeDec[j];
+        }
+        if (halt_round[j] == k) halted[j] = 1;
+        al[j] = P.val[j] & (1u - halted[j]);
+      }
+      act = P.ballot(al);
+    }
+    check(k + 1);
+  }
+  int32_t mainx[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) mainx[j] = P.val[j] ? kset_pick<W>(t[j], L.x0s, Emin, xmin) : 0;
+  pk_finish<W>(P, a, i, ck, 2, dec_val, dec_round, halt_round, mainx, bc);
+  lds_sync<1>();  // x0s / ts reads done before the next instance restages them
+}
+
+#ifndef PSG_KSET_PK_WPE
+#define PSG_KSET_PK_WPE 2  // W = 4 packs four 256-bit t masks (and their next values) per lane
+#endif
+template <int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_KSET_PK_WPE))) kset_packed_kernel(KArgs a) {
+  __shared__ BlockCounters bc;
+  __shared__ KsPk<W> L[4];
+  __shared__ int32_t x0tab[4][X0Set<W>::kSlots];
+  counters_init(&bc);
+  __syncthreads();
+  Pk<W> P;
+  P.setup(a.n);
+  const int grp = threadIdx.x >> 6;
+  InstanceQueue<1> Q;
+  for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
+    const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
+    kset_packed<W>(P, a, i, inst, L[grp], x0tab[grp], &bc);
+  }
+  __syncthreads();
+  counters_flush(&bc, a.counters, 2, a.R);
 }
 
 // Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
@@ -175,48 +435,7 @@ PSG_DEV void kset_body(const KArgs& a) {
         }
         if (adopt) {
           // t = content.find(_._1).get._2 — first decider message in iteration order
-          int qs = mfirst(cand);
-          if (a.tiebreak == PSG_TIE_CHAMP && mpopc(M) > 4 && mpopc(cand) > 1) {
-            const Mask<W> t0 = load_t<W>(ts, qs);
-            bool differ = false;
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-              uint64_t m = cand.w[w];
-              while (m) {
-                const int q = w * 64 + __builtin_ctzll(m);
-                m &= m - 1;
-                if (!meq(load_t<W>(ts, q), t0)) differ = true;
-              }
-            }
-            if (differ) {
-              uint64_t best = ~0ull;
-#pragma unroll
-              for (int w = 0; w < W; ++w) {
-                uint64_t m = cand.w[w];
-                while (m) {
-                  const int q = w * 64 + __builtin_ctzll(m);
-                  m &= m - 1;
-                  const uint32_t hq = scala_improve((uint32_t)q);
-                  int depth = 0;
-#pragma unroll
-                  for (int v = 0; v < W; ++v) {
-                    uint64_t mm = M.w[v];
-                    while (mm) {
-                      const int f = v * 64 + __builtin_ctzll(mm);
-                      mm &= mm - 1;
-                      if (f != q) depth = max(depth, champ_cpl(hq, scala_improve((uint32_t)f)));
-                    }
-                  }
-                  const uint64_t key = champ_key(hq, depth);
-                  if (key < best) {
-                    best = key;
-                    qs = q;
-                  }
-                }
-              }
-            }
-          }
-          tnew = load_t<W>(ts, qs);
+          tnew = load_t<W>(ts, kset_find<W>(a, ts, M, cand));
           becomeDecider = true;
         }
         if (!halted && isDec) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:48-50)
@@ -261,6 +480,13 @@ kset_kernel(KArgs a) {
 #ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
+  if constexpr (W > 1) {  // seeded schedule, built-in checker: lane-packed path
+    if (!a.ho_in && !a.trace) {
+      const int pg = pk_grid<PSG_ALG_KSET, W>((const void*)kset_packed_kernel<W>, a.count);
+      hipLaunchKernelGGL((kset_packed_kernel<W>), dim3(pg), dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
+  }
   if (a.ho_in) hipLaunchKernelGGL((kset_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   else hipLaunchKernelGGL((kset_kernel<W, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();

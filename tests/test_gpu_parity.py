@@ -50,6 +50,17 @@ CASES = [
     ("kset-n16-loss", psync.KSetAgreement(2), 16, 2000, dict(seed=23, schedule=H(drop_log2=2, good_round=0.0))),
     ("kset-n16-minpid", psync.KSetAgreement(2), 16, 2000, dict(seed=24, tiebreak=abi.PSG_TIE_MIN_PID,
                                                               schedule=H(drop_log2=2, good_round=0.0))),
+    # lane-packed KSet path (n > 64, seeded schedules): ragged n, every W, losses, good rounds,
+    # both Map tie-break modes (CHAMP find on divergent decider candidates), mutant
+    ("kset-n65-k2", psync.KSetAgreement(2), 65, 300, dict(seed=80)),
+    ("kset-n130-k3-loss", psync.KSetAgreement(3), 130, 150, dict(seed=81, schedule=H(drop_log2=2, good_round=0.0,
+                                                                                     crash_fmax=5))),
+    ("kset-n200-minpid", psync.KSetAgreement(2), 200, 100, dict(seed=82, tiebreak=abi.PSG_TIE_MIN_PID,
+                                                                schedule=H(drop_log2=1, good_round=0.3))),
+    ("kset-n256-k4-champ", psync.KSetAgreement(4), 256, 60, dict(seed=83, schedule=H(drop_log2=1, good_round=0.2,
+                                                                                      crash_fmax=3))),
+    ("kset-n192-mutant", psync.KSetAgreement(2, variant=1), 192, 100, dict(seed=84)),
+    ("kset-n256-k2-V3", psync.KSetAgreement(2), 256, 100, dict(seed=85, value_range=3)),
     ("benor-n128", psync.BenOr(), 128, 300, dict(seed=25)),
     ("benor-n4", psync.BenOr(), 4, 3000, dict(seed=26)),
     ("benor-n64-mutant", psync.BenOr(variant=1), 64, 500, dict(seed=27)),
@@ -139,8 +150,9 @@ def test_host_supplied_inputs(oracle_mod):
     assert [_inst_tuple(s) for s in res.per_instance] == [_inst_tuple(s) for s in opi]
 
 
-@pytest.mark.parametrize("alg,n", [(psync.FloodMin(5), 256), (psync.FloodMin(3), 100), (psync.BenOr(), 128)],
-                         ids=["fm-n256", "fm-n100", "benor-n128"])
+@pytest.mark.parametrize("alg,n", [(psync.FloodMin(5), 256), (psync.FloodMin(3), 100), (psync.BenOr(), 128),
+                                   (psync.KSetAgreement(2), 256), (psync.KSetAgreement(3), 90)],
+                         ids=["fm-n256", "fm-n100", "benor-n128", "kset-n256", "kset-n90"])
 def test_host_supplied_inputs_wide(alg, n, oracle_mod):
     """Caller-provided initial values on the wide fast paths (lane-packed kernels)."""
     count = 150
