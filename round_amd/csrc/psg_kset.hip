@@ -146,28 +146,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
   const Mask<W> Emin = P.ballot(emin);
   Checks ck;
   ck.reset();
-  // k-agreement (kagree_check): decisions of never-crashed deciders number <= k; every
-  // decision is an initial value
-  auto check = [&](int c) {
-    uint32_t dc[W], undec = 0, bad = 0;
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-      dc[j] = P.val[j] & decided[j] & (cr[j] >= 0 ? 0u : 1u);
-      undec |= P.val[j] & (1u - decided[j]);
-      bad |= P.val[j] & decided[j] & (1u - X0.contains01(decision[j]));
-    }
-    Mask<W> Y = P.ballot(dc);
-    int distinct = 0;
-    while (many(Y) && distinct <= kk) {
-      const int32_t dv = P.bcast(decision, mfirst(Y));
-      uint32_t eq[W];
-#pragma unroll
-      for (int j = 0; j < W; ++j) eq[j] = dc[j] & eq01(decision[j], dv);
-      Y = mandn(Y, P.ballot(eq));
-      ++distinct;
-    }
-    ck.record(fbit(distinct <= kk, 0) | fbit(!pk_any(bad), 1), !pk_any(undec), c, P.lane);
-  };
+  auto check = [&](int c) { pk_kagree_check<W>(P, ck, c, kk, decided, decision, cr, X0); };
   check(0);
   Mask<W> act;
   {

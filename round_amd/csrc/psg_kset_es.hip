@@ -11,6 +11,7 @@
 // never-crashed deciders and validity, like KSetAgreement.
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
+#include "psg_packed.hpp"
 
 namespace psg {
 
@@ -18,6 +19,141 @@ template <int W>
 struct EsLds {
   int32_t ds[W > 1 ? 64 * W : 1];
 };
+
+// ---------------------------------------------------------------- lane-packed path (n > 64)
+// kset_es_body's built-in-checker path, one wave per instance with the W processes
+// l + 64 j in lane l (psg_packed.hpp): the ascending walk over the distinct sender
+// estimates takes the wave minimum of the lane's minimum over its slots still in the
+// walk, and every ballot is a wave ballot (no block barrier per step).
+template <int W>
+PSG_DEV void kset_es_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, int32_t* x0lds,
+                            BlockCounters* bc) {
+  const int n = a.n, t = a.param, kk = a.param2;
+  Sched<W, false> sc;
+  sc.setup(a, inst, P.lane, false);
+  sc.prep_good(0, P.lane, a.R);
+  int32_t cr[W];
+  pk_crash_rounds<W>(P, a, inst, cr);
+  // KSetESProcess state after init(io) (KSetEarlyStopping.scala:16-21)
+  int32_t est[W], lastNb[W], decision[W], dec_val[W], dec_round[W], halt_round[W];
+  uint32_t cd[W], decided[W], halted[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    est[j] = 0;
+    if (P.val[j])
+      est[j] = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + P.pid(j)] : sc.init_value(P.pid(j), PSG_ALG_KSET_ES);
+    lastNb[j] = n;
+    decision[j] = dec_val[j] = 0;
+    dec_round[j] = halt_round[j] = -1;
+    cd[j] = decided[j] = 0;
+    halted[j] = 1u - P.val[j];
+  }
+  X0Set<W> X0;
+  pk_x0_build<W>(P, X0, x0lds, est);
+  Checks ck;
+  ck.reset();
+  auto check = [&](int c) { pk_kagree_check<W>(P, ck, c, kk, decided, decision, cr, X0); };
+  check(0);
+  for (int k = 0; k < a.R; ++k) {
+    uint32_t al[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) al[j] = 1u - halted[j];
+    const Mask<W> act = P.ballot(al);  // alive senders
+    if (many(act)) {
+      const Mask<W> CD = P.ballot(cd);  // senders' canDecide flags (pre-state)
+      Mask<W> goodS;
+      const bool good = sc.good_round(k, P.lane, a.R, goodS);
+      Mask<W> CB = mzero<W>(), CN = mzero<W>();
+      if (sc.crash_on) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          CB.w[j] = __builtin_amdgcn_ballot_w64(cr[j] >= 0 && cr[j] < k);
+          CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
+        }
+      }
+      Mask<W> M[W];
+      int32_t currNb[W], nest[W];
+      uint32_t anyCD[W], decideNow[W], unres[W], selfIn[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        M[j] = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
+        currNb[j] = mpopc(M[j]);
+        anyCD[j] = many(mand(M[j], CD)) ? 1u : 0u;  // mailbox.exists(_._2._2), pre-update flags
+        decideNow[j] = (1u - halted[j]) & ((k > t / kk) ? 1u : cd[j]);
+        // est = min over the mailbox's estimates (unchanged if the mailbox is empty)
+        unres[j] = (1u - halted[j]) & (1u - decideNow[j]) & (currNb[j] > 0 ? 1u : 0u);
+        selfIn[j] = (uint32_t)((M[j].w[j] >> P.lane) & 1ull);
+        nest[j] = est[j];
+      }
+      Mask<W> rem = act;
+      while (many(rem)) {
+        int32_t mn = INT32_MAX;
+        uint32_t anyU = 0;
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          if ((rem.w[j] >> P.lane) & 1ull) mn = min(mn, est[j]);
+          anyU |= unres[j];
+        }
+        if (!pk_any(anyU)) break;
+        const int32_t v = Grp<1>::dpp_reduce32<false>(mn);  // rem non-empty: a sender value
+        uint32_t eq[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) eq[j] = eq01(est[j], v);
+        const Mask<W> E = mand(P.ballot(eq), rem);
+        rem = mandn(rem, E);
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          if (unres[j]) {
+            if (many(mand(M[j], E))) {
+              nest[j] = v;
+              unres[j] = 0;
+            } else if (selfIn[j] && v >= est[j]) {
+              unres[j] = 0;  // nothing below the receiver's own estimate reached it
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        if (decideNow[j]) {  // callback.decide(est); exitAtEndOfRound (KSetEarlyStopping.scala:32-34)
+          dec_val[j] = est[j];
+          dec_round[j] = k;
+          decided[j] = 1;
+          decision[j] = est[j];
+          halt_round[j] = k;
+          halted[j] = 1;
+        } else if (!halted[j]) {  // KSetEarlyStopping.scala:36-38 (variant 1: mutation, always canDecide)
+          est[j] = nest[j];
+          cd[j] = a.variant == 1 ? 1u : ((anyCD[j] || lastNb[j] - currNb[j] < kk) ? 1u : 0u);
+          lastNb[j] = currNb[j];
+        }
+      }
+    }
+    check(k + 1);
+  }
+  pk_finish<W>(P, a, i, ck, 2, dec_val, dec_round, halt_round, est, bc);
+}
+
+#ifndef PSG_KSETES_PK_WPE
+#define PSG_KSETES_PK_WPE 5  // W = 4: 5 waves/SIMD (with some scratch) measured over 3 / 4: 17.2 vs 18.5 / 17.9 ms
+#endif
+template <int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_KSETES_PK_WPE)))
+kset_es_packed_kernel(KArgs a) {
+  __shared__ BlockCounters bc;
+  __shared__ int32_t x0tab[4][X0Set<W>::kSlots];
+  counters_init(&bc);
+  __syncthreads();
+  Pk<W> P;
+  P.setup(a.n);
+  InstanceQueue<1> Q;
+  for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
+    const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
+    kset_es_packed<W>(P, a, i, inst, x0tab[threadIdx.x >> 6], &bc);
+  }
+  __syncthreads();
+  counters_flush(&bc, a.counters, 2, a.R);
+}
 
 // Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
 // fused Spec module (round_amd/formula.py compile_native(fused=True)).
@@ -141,6 +277,13 @@ kset_es_kernel(KArgs a) {
 #ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
+  if constexpr (W > 1) {  // seeded schedule, built-in checker: lane-packed path
+    if (!a.ho_in && !a.trace) {
+      const int pg = pk_grid<PSG_ALG_KSET_ES, W>((const void*)kset_es_packed_kernel<W>, a.count);
+      hipLaunchKernelGGL((kset_es_packed_kernel<W>), dim3(pg), dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
+  }
   if (a.ho_in) hipLaunchKernelGGL((kset_es_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   else hipLaunchKernelGGL((kset_es_kernel<W, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();

@@ -111,6 +111,32 @@ PSG_DEV void pk_x0_build(const Pk<W>& P, X0Set<W>& X, int32_t* lds, const int32_
   lds_sync<1>();
 }
 
+// k-agreement over a packed instance (kagree_check): slot 0 — the decisions of never-
+// crashed deciders number <= k; slot 1 — every decision is an initial value; termination
+// when every process decided.
+template <int W>
+PSG_DEV void pk_kagree_check(const Pk<W>& P, Checks& ck, int c, int kk, const uint32_t (&decided)[W],
+                             const int32_t (&decision)[W], const int32_t (&cr)[W], const X0Set<W>& X0) {
+  uint32_t dc[W], undec = 0, bad = 0;
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    dc[j] = P.val[j] & decided[j] & (cr[j] >= 0 ? 0u : 1u);
+    undec |= P.val[j] & (1u - decided[j]);
+    bad |= P.val[j] & decided[j] & (1u - X0.contains01(decision[j]));
+  }
+  Mask<W> Y = P.ballot(dc);
+  int distinct = 0;
+  while (many(Y) && distinct <= kk) {
+    const int32_t dv = P.bcast(decision, mfirst(Y));
+    uint32_t eq[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) eq[j] = dc[j] & eq01(decision[j], dv);
+    Y = mandn(Y, P.ballot(eq));
+    ++distinct;
+  }
+  ck.record(fbit(distinct <= kk, 0) | fbit(!pk_any(bad), 1), !pk_any(undec), c, P.lane);
+}
+
 // Per-instance epilogue of a packed instance (finish_instance for W slots per lane):
 // the same digest (a sum over processes), decide results, summaries and counters.
 template <int W>

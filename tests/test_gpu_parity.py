@@ -91,6 +91,14 @@ CASES = [
     ("kses-n64-t8k2", psync.KSetEarlyStopping(8, 2), 64, 1000, dict(seed=49)),
     ("kses-n256-t16k3", psync.KSetEarlyStopping(16, 3), 256, 100, dict(seed=50)),
     ("kses-mutant-n16", psync.KSetEarlyStopping(4, 2, variant=1), 16, 3000, dict(seed=51)),
+    # lane-packed KSetEarlyStopping path (n > 64, seeded schedules)
+    ("kses-n65-t8k2", psync.KSetEarlyStopping(8, 2), 65, 300, dict(seed=90)),
+    ("kses-n130-loss", psync.KSetEarlyStopping(16, 3), 130, 150, dict(seed=91, schedule=H(
+        drop_log2=2, good_round=0.2, crash_fmax=10))),
+    ("kses-n200-pureho", psync.KSetEarlyStopping(8, 2), 200, 100, dict(seed=92, schedule=H(
+        drop_log2=1, good_round=0.0, crash_fmax=6, self_bit=False))),
+    ("kses-n256-mutant", psync.KSetEarlyStopping(16, 2, variant=1), 256, 60, dict(seed=93)),
+    ("kses-n192-t64k2", psync.KSetEarlyStopping(64, 2), 192, 60, dict(seed=94)),
     ("kses-pureho", psync.KSetEarlyStopping(4, 2), 16, 2000, dict(seed=52, schedule=H(
         drop_log2=2, good_round=0.0, crash_fmax=4, self_bit=False))),
 ]
@@ -151,8 +159,9 @@ def test_host_supplied_inputs(oracle_mod):
 
 
 @pytest.mark.parametrize("alg,n", [(psync.FloodMin(5), 256), (psync.FloodMin(3), 100), (psync.BenOr(), 128),
-                                   (psync.KSetAgreement(2), 256), (psync.KSetAgreement(3), 90)],
-                         ids=["fm-n256", "fm-n100", "benor-n128", "kset-n256", "kset-n90"])
+                                   (psync.KSetAgreement(2), 256), (psync.KSetAgreement(3), 90),
+                                   (psync.KSetEarlyStopping(16, 2), 256)],
+                         ids=["fm-n256", "fm-n100", "benor-n128", "kset-n256", "kset-n90", "kses-n256"])
 def test_host_supplied_inputs_wide(alg, n, oracle_mod):
     """Caller-provided initial values on the wide fast paths (lane-packed kernels)."""
     count = 150
