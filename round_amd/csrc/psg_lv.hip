@@ -10,6 +10,10 @@
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
 
+#ifndef PSG_LV_EXP
+#define PSG_LV_EXP 0  // timing experiments only (1: no majority scan, 2: check reduced to termination)
+#endif
+
 namespace psg {
 
 // per-process flag bits (one VGPR word; see nz01 in psg_device.hpp)
@@ -45,13 +49,27 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, const X0Set<W>& X0, Checks& ck, in
   lv_stage<W>(g, L, x, ts, vote, decision);
   const int32_t r4 = c / 4;
   const int coord = r4 % n;
-  const Mask<W> D = g.ballot((fl & F_DECIDED) != 0u);
+  const uint32_t dec01 = (fl & F_DECIDED) ? 1u : 0u;
+  const Mask<W> D = g.ballot(dec01 != 0u);
   const Mask<W> C = g.ballot((fl & F_COMMIT) != 0u);
   const Mask<W> Rd = g.ballot((fl & F_READY) != 0u);
   const bool anyD = many(D);
   const int32_t d0 = anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
-  const bool same = !many(mand(D, g.ballot(decision != d0)));
-  const bool keep = X0.all_in(g, full, x);  // P.forall(i => P.exists(j1 => i.x == init(j1.x)))
+  if (PSG_LV_EXP == 2) { ck.record(0, meq(D, full), c, g.lane); return; }
+  // Agreement, keepInit, Validity and Irrevocability from one ballot of a per-process
+  // witness word (decision != d0; x or a decision maybe not initial — the X0 set's two
+  // home slots; a changed decision), resolved formula by formula only when some process
+  // may be a witness
+  uint32_t wit = (dec01 & (ne01(decision, d0) | X0.maybe_out01(decision))) | X0.maybe_out01(x);
+  if (has_old) wit |= ((old_fl & F_DECIDED) ? 1u : 0u) & (1u - (dec01 & eq01(old_decision, decision)));
+  bool same = true, keep = true, validity = true, irrev = true;
+  if (g.any(wit != 0u)) {
+    same = !many(mand(D, g.ballot(decision != d0)));
+    keep = X0.all_in(g, full, x);  // P.forall(i => P.exists(j1 => i.x == init(j1.x)))
+    validity = X0.all_in(g, D, decision);
+    const Mask<W> OLD = g.ballot((old_fl & F_DECIDED) != 0u);
+    irrev = !has_old || !many(mandn(OLD, mand(D, g.ballot(old_decision == decision))));
+  }
   const bool noDec = !many(mor(D, Rd));
   // values pinned by (decided ==> decision == v), (commit ==> vote == v), (ready ==> vote == v)
   const Mask<W> CR = mor(C, Rd);
@@ -61,48 +79,38 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, const X0Set<W>& X0, Checks& ck, in
   bool zOk = true;
   if (zAny) {
     const int q = mfirst(Pm);
-    z0 = mtest(D, q) ? g.bcast(decision, L.ds, q) : g.bcast(vote, L.votes, q);
-    zOk = !many(mor(mand(D, g.ballot(decision != z0)), mand(CR, g.ballot(vote != z0))));
+    const bool qD = mtest(D, q);  // then q is also the first decider: z0 = d0
+    z0 = qD ? d0 : g.bcast(vote, L.votes, q);
+    // the deciders' part is empty when every decision equals d0 = z0 (or nobody decided)
+    const Mask<W> zd = (same && (qD || !anyD)) ? mzero<W>() : mand(D, g.ballot(decision != z0));
+    zOk = !many(mor(zd, mand(CR, g.ballot(vote != z0))));
   }
   const bool c5 = mtest(C, coord) || !g.any(ts == r4);  // (i.ts == r/4) ==> coord.commit
   bool maj = false;
-  if (c > 0 && zOk && c5) {
+  if (PSG_LV_EXP != 1 && c > 0 && zOk && c5) {
     // exists t <= r/4: A_t = {i : i.ts >= t}, |A_t| > n/2, all x over A_t equal (to the pinned
     // value). The sets A_t shrink as t grows, and "all x over A equal (to z0)" holds on every
     // non-empty subset of a set it holds on, so the exists holds iff it holds at the largest
-    // t <= r/4 with |A_t| > n/2: the (n/2+1)-th largest min(ts, r/4). Scan the distinct values
-    // of min(ts, r/4) from the top (max by ballot descent over the bits of ts+1 in [0, r/4+1])
-    // until the count passes n/2.
+    // t <= r/4 with |A_t| > n/2. With tv = min(ts, r/4) + 1 in [0, r/4 + 1] that is the
+    // largest u with |{tv >= u}| > n/2 (a present value; u = 0 always qualifies): a binary
+    // search on the count, ceil(log2(r/4 + 2)) ballots.
     const int32_t tsc = ts < r4 ? ts : r4;
     const uint32_t tv = (uint32_t)(tsc + 1);  // ts >= -1 (LastVoting.scala:87)
-    const int bits = 32 - __builtin_clz((uint32_t)(r4 + 1) | 1u);
-    Mask<W> below = full;  // processes under every value scanned so far
-    Mask<W> A;
-    for (;;) {
-      Mask<W> cand = below;
-      uint32_t u = 0;
-      for (int b = bits - 1; b >= 0; --b) {
-        const Mask<W> m = mand(cand, g.ballot((tv >> b) & 1u));
-        if (many(m)) {
-          cand = m;
-          u |= 1u << b;
-        }
-      }
-      A = g.ballot(tv >= u);
-      if (mpopc(A) > n / 2) break;
-      below = mandn(full, A);
+    uint32_t lo = 0, hi = (uint32_t)r4 + 2u;
+    while (hi - lo > 1u) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (mpopc(g.ballot(tv >= mid)) > n / 2) lo = mid;
+      else hi = mid;
     }
+    const Mask<W> A = g.ballot(tv >= lo);
     const int32_t xv = g.bcast(x, L.xs, mfirst(A));
     maj = !many(mand(A, g.ballot(x != xv))) && (!zAny || xv == z0);
   }
   const bool inv0 = keep && (noDec || maj);
-  const bool validity = X0.all_in(g, D, decision);
   const bool d0in = same && validity;
   const bool term = meq(D, full);
   const bool inv1 = term && d0in;
   const bool integrity = !anyD || d0in;
-  const Mask<W> OLD = g.ballot((old_fl & F_DECIDED) != 0u);
-  const bool irrev = !has_old || !many(mandn(OLD, mand(D, g.ballot(old_decision == decision))));
   const uint32_t fb = fbit(inv0 || inv1, 0) | fbit(inv0, 1) | fbit(inv1, 2) | fbit(same, 3) | fbit(validity, 4) |
                       fbit(integrity, 5) | fbit(irrev, 6);
   ck.record(fb, term, c, g.lane);
