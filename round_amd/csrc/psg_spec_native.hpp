@@ -143,6 +143,48 @@ PSG_DEV int32_t quant_tup(Ctx<W>& x, Fn fn, Fs...) {
   return acc;
 }
 
+// The distinct-state quantifier's tuple, when every process holds the same one (per
+// check point, shared by the quantifiers over that field tuple): then quant_tup has one
+// iteration and needs no ballots — forall / exists give the body's value at the tuple,
+// count gives n or 0. (Settled states: every process decided the same value; early
+// rounds: nobody decided.)
+template <int NF>
+struct TupU {
+  bool uni;
+  int32_t v[NF];
+};
+
+template <int W, class... Fs>
+PSG_DEV TupU<(int)sizeof...(Fs)> tup_uniform(Ctx<W>& x, Fs...) {
+  TupU<(int)sizeof...(Fs)> t;
+  uint32_t diff = 0;
+  int k = 0;
+  auto one = [&](auto fld) {
+    using FL = decltype(fld);
+    const int32_t mine = x.own(FL::tag, FL::f);
+    t.v[k] = x.g.bcast(mine, x.stage(FL::tag, FL::f), 0);  // process 0 (n >= 1)
+    diff |= ne01(mine, t.v[k]);
+    ++k;
+  };
+  (one(Fs{}), ...);
+  t.uni = !x.g.any(diff != 0u);
+  return t;
+}
+
+template <int W, int MODE, int NF, class Fn, class... Fs>
+PSG_DEV int32_t quant_tup_c(Ctx<W>& x, const TupU<NF>& tu, Fn fn, Fs... fs) {
+  if (tu.uni) {
+    int32_t b;
+    if constexpr (NF == 1) b = fn(tu.v[0]);
+    else if constexpr (NF == 2) b = fn(tu.v[0], tu.v[1]);
+    else if constexpr (NF == 3) b = fn(tu.v[0], tu.v[1], tu.v[2]);
+    else b = fn(tu.v[0], tu.v[1], tu.v[2], tu.v[3]);
+    if constexpr (MODE == 2) return b != 0 ? x.n : 0;
+    else return b != 0 ? 1 : 0;
+  }
+  return quant_tup<W, MODE>(x, fn, fs...);
+}
+
 // P.exists(j => init(j.f) == t): membership of t in the instance's set of initial
 // values of f — an LDS hash set built once per instance (X0Set), as the
 // hand-lowered checks do, instead of a loop over the processes.

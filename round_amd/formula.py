@@ -718,6 +718,8 @@ class _Gen:
         self.tuples = {}      # var uid -> {(field, tag): C++ name} (serial quantifier over distinct states)
         self.init_sets = []   # fields f with an LDS membership set of init(f) (at most 2)
         self.cse = {}         # id(closed subformula) -> C++ name of its hoisted value
+        self.tup_sets = {}    # field tuple of a distinct-state quantifier -> C++ name of its per-check-point TupU
+        self.tup_used = set()  # field tuples used by the function being generated
 
     def gen(self, e, in_lane, vi_depth):
         """(C++ expression, depends on the lane)."""
@@ -813,8 +815,15 @@ class _Gen:
                 mode = {"forall": 0, "exists": 1, "count": 2}[q.kind]
                 params = ", ".join(f"int32_t {names[ft]}" for ft in flds)
                 fl = ", ".join(f"spec::Fld<{f}, {tag}>{{}}" for f, tag in flds)
-                return (f"spec::quant_tup<W, {mode}>(x, [&]({params}) -> int32_t {{ return {body}; }}"
-                        f"{', ' if fl else ''}{fl})"), lane
+                if not flds:
+                    return (f"spec::quant_tup<W, {mode}>(x, [&]({params}) -> int32_t {{ return {body}; }})"), lane
+                # per check point: are those fields the same for every process (one tuple)?
+                key = tuple(flds)
+                if key not in self.tup_sets:
+                    self.tup_sets[key] = f"tu{len(self.tup_sets)}"
+                self.tup_used.add(key)
+                return (f"spec::quant_tup_c<W, {mode}>(x, {self.tup_sets[key]}, [&]({params}) -> int32_t "
+                        f"{{ return {body}; }}, {fl})"), lane
             self.names[q.var.uid] = (v, False, False)
             body, lane = self.gen(q.body, in_lane, vi_depth)
             fn = {"forall": "forall_ser", "exists": "exists_ser", "count": "count_ser"}[q.kind]
@@ -1099,9 +1108,12 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
             lines.append(f"    if (inv{k} == 0) fb |= 1u << {slot};")
             slot += 1
     term = None
+    term_tups = set()
     for name, f in props:
         if name == "Termination":
+            saved, gen.tup_used = gen.tup_used, set()
             term, _ = gen.gen(f, False, 0)
+            term_tups, gen.tup_used = gen.tup_used, saved
             continue
         c, _ = gen.gen(f, False, 0)
         lines.append(f"    if (({c}) == 0) fb |= 1u << {slot};  // {name}")
@@ -1113,6 +1125,11 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
     assert slot == len(prog.slot_entry)
     if gen.max_vi > 4:
         raise FormulaError("more than 4 nested V.exists over Int")
+    def tup_decls(used):
+        return [f"    const auto {gen.tup_sets[k]} = spec::tup_uniform<W>(x, "
+                + ", ".join(f"spec::Fld<{f}, {tag}>{{}}" for f, tag in k) + ");"
+                for k in gen.tup_sets if k in used]
+    lines = tup_decls(gen.tup_used) + lines
     rel = sum(1 << s for s, fl in enumerate(prog.slot_flags) if fl & SPEC_RELATIONAL)
     fmask = sum(1 << f for f in gen.fields)
     tmask = sum(1 << t for t in gen.tags)
@@ -1138,6 +1155,7 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
         "  template <int W>",
         "  __device__ static bool term(spec::Ctx<W>& x, int32_t* scratch) {",
         "    (void)scratch;",
+        *tup_decls(term_tups),
         f"    return ({term or '0'}) != 0;",
         "  }",
         "};",
