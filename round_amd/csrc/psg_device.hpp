@@ -1213,6 +1213,19 @@ struct X0Set {
     const int32_t t1 = tab[(h + 1) & (uint32_t)(kSlots - 1)];
     return (ne01(t0, v) & ne01(t1, v)) | eq01(v, kEmpty);
   }
+  // maybe_out01 of two values under one test of the mode (one scalar branch, not two)
+  PSG_DEV void maybe_out01_2(int32_t a, int32_t b, uint32_t& oa, uint32_t& ob) const {
+    if (bmode) {
+      oa = 1u - bm_in01(a);
+      ob = 1u - bm_in01(b);
+      return;
+    }
+    const uint32_t ha = slot(a), hb = slot(b);
+    const int32_t a0 = tab[ha], a1 = tab[(ha + 1) & (uint32_t)(kSlots - 1)];
+    const int32_t b0 = tab[hb], b1 = tab[(hb + 1) & (uint32_t)(kSlots - 1)];
+    oa = (ne01(a0, a) & ne01(a1, a)) | eq01(a, kEmpty);
+    ob = (ne01(b0, b) & ne01(b1, b)) | eq01(b, kEmpty);
+  }
   // contains() as a VALU 0/1 integer (see nz01); same probing scheme
   PSG_DEV uint32_t contains01(int32_t v) const {
     if (bmode) return bm_in01(v);
