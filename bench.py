@@ -222,7 +222,7 @@ def main():
                 "unit": "G SALU instructions/s",
                 "frac": None,
                 "traffic": None,
-                "kernel": "psg::otr_kernel<1, false, false, psg::NoHook>",  # <W, OTR2, explicit schedule, check hook>
+                "kernel": "psg::otr_kernel<1, false, false, psg::NoHook, false>",  # <W, OTR2, explicit schedule, hook, trace>
                 "kernel_ms": head["kernel_s"] * 1e3,
                 "hbm_algorithmic": {
                     "note": "SURVEY §8d accounting: 24 B of state per process-round as if streamed each "

@@ -98,9 +98,11 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
 }
 
 // Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
-// fused Spec module (round_amd/formula.py compile_native(fused=True)).
-template <int W, bool V2, bool XHO, class SH = NoHook>
+// fused Spec module (round_amd/formula.py compile_native(fused=True)). TR = false: the
+// launch has no Spec-program trace (a.trace == nullptr), known at compile time.
+template <int W, bool V2, bool XHO, class SH = NoHook, bool TR = true>
 PSG_DEV void otr_body(const KArgs& a) {
+  const bool tracing_on = SH::kFused || (TR && a.trace != nullptr);
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int32_t crl[W > 1 ? 64 * W : 1];
@@ -143,7 +145,7 @@ PSG_DEV void otr_body(const KArgs& a) {
     auto trace = [&](int c, int32_t hs) {
       emit_state<W, SH>(sh, g, a, i, c, x, (int32_t)dec01, V2 && !dec01 ? PSG_NONE32 : decision, 0, 0, 0, 0, 0, hs);
     };
-    if (tracing<SH>(a)) trace(0, n);
+    if (tracing_on) trace(0, n);
     pt.mark(0);
 
     for (int k = 0; k < a.R; ++k) {
@@ -159,7 +161,7 @@ PSG_DEV void otr_body(const KArgs& a) {
         // mailbox: broadcast(x) from every alive sender in HO(p)
         const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const int32_t msize = mpopc(M);
-        if (tracing<SH>(a)) hs = halted01 ? n : msize;
+        if (tracing_on) hs = halted01 ? n : msize;
         const uint32_t upd = (1u - halted01) & gt01(msize, thr);
         if (g.any(upd != 0u)) {
           // mmor: max multiplicity, ties -> smaller value (OtrExample.scala:67-75).
@@ -201,7 +203,7 @@ PSG_DEV void otr_body(const KArgs& a) {
         halted01 |= h;
       }
       if constexpr (!SH::kFused) otr_check<W, V2>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, old01, old_decision, valid01);
-      if (tracing<SH>(a)) trace(k + 1, hs);
+      if (tracing_on) trace(k + 1, hs);
       pt.mark(many(act) ? 1 : 2);
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 8, dec_val, dec_round, halt_round, x, &bc);
@@ -215,17 +217,18 @@ PSG_DEV void otr_body(const KArgs& a) {
 #ifndef PSG_OTR_WPE
 #define PSG_OTR_WPE 6
 #endif
-template <int W, bool V2, bool XHO, class SH = NoHook>
+template <int W, bool V2, bool XHO, class SH = NoHook, bool TR = true>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? PSG_OTR_WPE : 1)))
 otr_kernel(KArgs a) {
-  otr_body<W, V2, XHO, SH>(a);
+  otr_body<W, V2, XHO, SH, TR>(a);
 }
 
 #ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W, bool V2>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
   if (a.ho_in) hipLaunchKernelGGL((otr_kernel<W, V2, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
-  else hipLaunchKernelGGL((otr_kernel<W, V2, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  else if (a.trace) hipLaunchKernelGGL((otr_kernel<W, V2, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  else hipLaunchKernelGGL((otr_kernel<W, V2, false, NoHook, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -243,10 +246,10 @@ static hipError_t launch_v(const KArgs& a, int W, int grid, hipStream_t s) {
 template <bool V2>
 static const void* ptr_v(int W) {
   switch (W) {
-    case 1: return (const void*)otr_kernel<1, V2, false>;
-    case 2: return (const void*)otr_kernel<2, V2, false>;
-    case 3: return (const void*)otr_kernel<3, V2, false>;
-    case 4: return (const void*)otr_kernel<4, V2, false>;
+    case 1: return (const void*)otr_kernel<1, V2, false, NoHook, false>;
+    case 2: return (const void*)otr_kernel<2, V2, false, NoHook, false>;
+    case 3: return (const void*)otr_kernel<3, V2, false, NoHook, false>;
+    case 4: return (const void*)otr_kernel<4, V2, false, NoHook, false>;
   }
   return nullptr;
 }

@@ -17,7 +17,7 @@ import shutil
 ap = argparse.ArgumentParser()
 ap.add_argument("src", help="gpurun_out/<tag> directory")
 ap.add_argument("dst", help="profiles/<tag> directory")
-ap.add_argument("--kernel", default="otr_kernel<1, false, false, psg::NoHook>")
+ap.add_argument("--kernel", default="otr_kernel<1, false, false, psg::NoHook, false>")
 ap.add_argument("--process-rounds", type=float, default=1e7 * 64 * 20, help="process-rounds per launch")
 ap.add_argument("--bytes-per-pr", type=float, default=24.0)
 args = ap.parse_args()
