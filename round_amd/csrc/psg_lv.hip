@@ -42,10 +42,12 @@ PSG_DEV void lv_stage(Grp<W>& g, LvLds<W>& L, int32_t x, int32_t ts, int32_t vot
 // Spec check at check point c (spec r = c). Slots: 0 Safety, 1 Invariant0
 // (keepInit && (noDecision || majority)), 2 Invariant1, 3 Agreement, 4 Validity,
 // 5 Integrity, 6 Irrevocability. roundInvariants(j-1)(0) is `true` for every j.
+// xin01 / din01: 1 iff x / decision is an initial value (tracked by the round step: x and
+// decision only ever take the coordinator's uniform vote, whose membership is probed once).
 template <int W>
-PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, const X0Set<W>& X0, Checks& ck, int c, bool has_old, int n,
-                      const Mask<W>& full, int32_t x, int32_t ts, int32_t vote, int32_t decision, uint32_t fl,
-                      uint32_t old_fl, int32_t old_decision) {
+PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, bool has_old, int n, const Mask<W>& full,
+                      int32_t x, int32_t ts, int32_t vote, int32_t decision, uint32_t fl, uint32_t old_fl,
+                      int32_t old_decision, uint32_t xin01, uint32_t din01) {
   lv_stage<W>(g, L, x, ts, vote, decision);
   const int32_t r4 = c / 4;
   const int coord = r4 % n;
@@ -57,16 +59,15 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, const X0Set<W>& X0, Checks& ck, in
   const int32_t d0 = anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
   if (PSG_LV_EXP == 2) { ck.record(0, meq(D, full), c, g.lane); return; }
   // Agreement, keepInit, Validity and Irrevocability from one ballot of a per-process
-  // witness word (decision != d0; x or a decision maybe not initial — the X0 set's two
-  // home slots; a changed decision), resolved formula by formula only when some process
-  // may be a witness
-  uint32_t wit = (dec01 & (ne01(decision, d0) | X0.maybe_out01(decision))) | X0.maybe_out01(x);
+  // witness word (decision != d0; x or a decision not initial; a changed decision),
+  // resolved formula by formula only when some process is a witness
+  uint32_t wit = (dec01 & (ne01(decision, d0) | (1u - din01))) | (1u - xin01);
   if (has_old) wit |= ((old_fl & F_DECIDED) ? 1u : 0u) & (1u - (dec01 & eq01(old_decision, decision)));
   bool same = true, keep = true, validity = true, irrev = true;
   if (g.any(wit != 0u)) {
     same = !many(mand(D, g.ballot(decision != d0)));
-    keep = X0.all_in(g, full, x);  // P.forall(i => P.exists(j1 => i.x == init(j1.x)))
-    validity = X0.all_in(g, D, decision);
+    keep = !many(mand(full, g.ballot(xin01 == 0u)));  // P.forall(i => P.exists(j1 => i.x == init(j1.x)))
+    validity = !many(mand(D, g.ballot(din01 == 0u)));
     const Mask<W> OLD = g.ballot((old_fl & F_DECIDED) != 0u);
     irrev = !has_old || !many(mandn(OLD, mand(D, g.ballot(old_decision == decision))));
   }
@@ -87,7 +88,8 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, const X0Set<W>& X0, Checks& ck, in
   }
   const bool c5 = mtest(C, coord) || !g.any(ts == r4);  // (i.ts == r/4) ==> coord.commit
   bool maj = false;
-  if (PSG_LV_EXP != 1 && c > 0 && zOk && c5) {
+  // (Invariant0 reads maj only when keepInit holds and some process decided or is ready)
+  if (PSG_LV_EXP != 1 && c > 0 && zOk && c5 && keep && !noDec) {
     // exists t <= r/4: A_t = {i : i.ts >= t}, |A_t| > n/2, all x over A_t equal (to the pinned
     // value). The sets A_t shrink as t grows, and "all x over A equal (to z0)" holds on every
     // non-empty subset of a set it holds on, so the exists holds iff it holds at the largest
@@ -206,11 +208,12 @@ PSG_DEV void lv_body(const KArgs& a) {
     // LVProcess state after init(io) (LastVoting.scala:82-109)
     int32_t x = x0, ts = -1, vote = 0, decision = -1;
     uint32_t fl = g.valid ? 0u : F_HALTED;
+    uint32_t xin = 1u, din = 1u;  // x / decision is an initial value (lv_check)
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
     Checks ck;
     ck.reset();
     typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
-    if constexpr (!SH::kFused) lv_check<W>(g, L, X0, ck, 0, false, n, full, x, ts, vote, decision, fl, 0u, -1);
+    if constexpr (!SH::kFused) lv_check<W>(g, L, ck, 0, false, n, full, x, ts, vote, decision, fl, 0u, -1, xin, din);
     auto trace = [&](int c, int32_t hs) {
       emit_state<W, SH>(sh, g, a, i, c, x, (fl & F_DECIDED) ? 1 : 0, decision, ts, (fl & F_READY) ? 1 : 0,
                    (fl & F_COMMIT) ? 1 : 0, vote, 0, hs);
@@ -235,10 +238,13 @@ PSG_DEV void lv_body(const KArgs& a) {
         // R1 / R3 read bit coord of every HO(p) (a mailbox of at most the coordinator's
         // message); R0 / R2 only HO(coord)
         const bool coordRound = (k & 1) == 0;
+        // R1 / R3: does the coordinator send (commit / ready, LastVoting.scala:141, 187)? When it
+        // does not, no mailbox is read and no HO bit of the round is observed
+        const bool sent = !coordRound && cAlive && mtest(g.ballot((fl & ((k & 3) == 1 ? F_COMMIT : F_READY)) != 0u), c);
         Mask<W> HO = mzero<W>(), HOc = mzero<W>();
         if constexpr (XHO) {
           HO = sc.ho(k, g.pid, good, goodS, CB, CN);
-        } else if (!coordRound) {
+        } else if (sent) {
           // only bit coord of HO(p) is read: the crash-round survival words matter only
           // when the coordinator crashes in this round, or when |HO(p)| decides the
           // ho_min rule (other bits are left unspecified otherwise)
@@ -268,12 +274,13 @@ PSG_DEV void lv_body(const KArgs& a) {
             break;
           }
           case 1: {  // R1: coord broadcasts vote if commit; receivers adopt (x, ts = r/4)
-            const bool sent = cAlive && mtest(g.ballot((fl & F_COMMIT) != 0u), c);
             hs = sent && mtest(HO, c) ? 1 : 0;
             if (sent) {
               const int32_t vc = g.bcast(vote, L.votes, c);
               const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
+              const uint32_t vin = SH::kFused ? 1u : X0.contains01(vc);  // one probe of a uniform value
               x = rcv ? vc : x;
+              xin = rcv ? vin : xin;
               ts = rcv ? phase : ts;
             }
             break;
@@ -285,11 +292,12 @@ PSG_DEV void lv_body(const KArgs& a) {
             break;
           }
           default: {  // R3: coord broadcasts vote if ready; receivers decide and exit
-            const bool sent = cAlive && mtest(g.ballot((fl & F_READY) != 0u), c);
             hs = sent && mtest(HO, c) ? 1 : 0;
             if (sent) {
               const int32_t vc = g.bcast(vote, L.votes, c);
               const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
+              const uint32_t vin = SH::kFused ? 1u : X0.contains01(vc);
+              din = rcv ? vin : din;
               const uint32_t first = rcv & (dec_round < 0 ? 1u : 0u);
               dec_val = first ? vc : dec_val;
               dec_round = first ? k : dec_round;
@@ -304,7 +312,7 @@ PSG_DEV void lv_body(const KArgs& a) {
         }
         pt.mark(2);
       }
-      if constexpr (!SH::kFused) lv_check<W>(g, L, X0, ck, k + 1, true, n, full, x, ts, vote, decision, fl, old_fl, old_decision);
+      if constexpr (!SH::kFused) lv_check<W>(g, L, ck, k + 1, true, n, full, x, ts, vote, decision, fl, old_fl, old_decision, xin, din);
       if (tracing<SH>(a)) trace(k + 1, (old_fl & F_HALTED) ? n : hs);
       pt.mark(many(act) ? 4 : 5);
     }

@@ -1215,7 +1215,7 @@ def compile_native(spec: Spec, alg: Optional[int] = None, cache_dir: str = None,
             raise FormulaError("fused lowering needs one of the integer-state algorithms")
         waves = [(n + 63) // 64] if n is not None else [1, 2, 3, 4]
         src = "#define PSG_FUSED_MODULE 1\n" + src + _fused_source(alg, waves)
-        hdr_names.append(FUSED_KERNELS[alg][0])
+        hdr_names += [FUSED_KERNELS[alg][0], "psg_kernels.hpp", "psg_packed.hpp"]  # everything it includes
     cache_dir = cache_dir or CACHE_DIR
     os.makedirs(cache_dir, exist_ok=True)
     hdrs = "".join(open(os.path.join(_CSRC, h)).read() for h in hdr_names)
