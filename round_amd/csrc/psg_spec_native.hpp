@@ -243,6 +243,7 @@ struct ExistsInt {
     const int32_t b = fn(cand);
     acc = (acc != 0 || b != 0) ? 1 : 0;
   }
+  uint32_t shifts = 7u;  // breakpoint mode (exists_int_bp): bit d+1 -> test v + d, d in {-1, 0, 1}
   PSG_DEV void visit(int32_t v) {
     if constexpr (EQ) {
       test(v);
@@ -250,7 +251,8 @@ struct ExistsInt {
       hi = any_v && hi > v ? hi : v;
       any_v = true;
     } else {
-      for (int d = -1; d <= 1; ++d) test((int32_t)((uint32_t)v + (uint32_t)d));
+      for (int d = -1; d <= 1; ++d)
+        if ((shifts >> (d + 1)) & 1u) test((int32_t)((uint32_t)v + (uint32_t)d));
     }
   }
   // distinct values of the per-lane `val` over the lanes in `m`
@@ -267,9 +269,11 @@ struct ExistsInt {
 
 template <int W, int NE, int NF, class Fn, bool EQ>
 PSG_DEV bool exists_int_scan(ExistsInt<W, Fn, EQ>& e, Ctx<W>& x, const int32_t (&ev)[NE > 0 ? NE : 1],
-                             const int32_t (&fs)[NF > 0 ? NF : 1], int32_t* scratch) {
+                             const int32_t (&fs)[NF > 0 ? NF : 1], int32_t* scratch,
+                             const uint32_t* shifts = nullptr) {
   const Mask<W> all = x.g.ballot(true);
   for (int k = 0; k < NE; ++k) {
+    if (shifts) e.shifts = shifts[k];
     if constexpr (W > 1) {
       scratch[x.g.pid] = ev[k];
       __syncthreads();
@@ -279,6 +283,7 @@ PSG_DEV bool exists_int_scan(ExistsInt<W, Fn, EQ>& e, Ctx<W>& x, const int32_t (
     if (d) return true;
   }
   for (int k = 0; k < NF; ++k) {
+    if (shifts) e.shifts = shifts[NE + k];
     const int f = fs[k] & 0xff, tag = (fs[k] >> 8) & 0xff;
     if (e.over(x.own(tag, f), all, x.stage(tag, f))) return true;
   }
@@ -291,6 +296,20 @@ PSG_DEV int32_t exists_int(Ctx<W>& x, const int32_t (&ev)[NE > 0 ? NE : 1], cons
   ExistsInt<W, Fn, false> e{x, fn, 0, 0, 0, false};
   if (exists_int_scan<W, NE, NF>(e, x, ev, fs, scratch)) return e.acc;
   e.test(INT32_MIN);
+  e.test(INT32_MAX);
+  return e.acc;
+}
+
+// V.exists over Int by breakpoints: every atom of the body that reads the variable t is
+// `t <= b` or its negation for a breakpoint b of its compared term e (t <= e, t > e: b = e;
+// t < e, t >= e: b = e - 1; t == e, t != e: both), so the body is constant on each interval
+// (b_j, b_j+1] and on (b_max, Int.MaxValue]: the breakpoints (right ends) plus Int.MaxValue
+// decide it. shifts[k] (bit d+1: b = e + d) per candidate source, sources as exists_int.
+template <int W, int NE, int NF, class Fn>
+PSG_DEV int32_t exists_int_bp(Ctx<W>& x, const int32_t (&ev)[NE > 0 ? NE : 1], const int32_t (&fs)[NF > 0 ? NF : 1],
+                              const uint32_t (&shifts)[NE + NF > 0 ? NE + NF : 1], int32_t* scratch, Fn fn) {
+  ExistsInt<W, Fn, false> e{x, fn, 0, 0, 0, false};
+  if (exists_int_scan<W, NE, NF>(e, x, ev, fs, scratch, shifts)) return e.acc;
   e.test(INT32_MAX);
   return e.acc;
 }

@@ -898,11 +898,17 @@ class _Gen:
         ne, nf = len(evs), len(fsets)
         ev = ", ".join(evs) if evs else "0"
         fs = ", ".join(str(f | (t << 8)) for f, t in fsets) if fsets else "0"
-        fn = "exists_int_eq" if eq_only else "exists_int"
-        return (f"([&]() -> int32_t {{ const int32_t ev_[{max(ne, 1)}] = {{{ev}}}; "
-                f"const int32_t fs_[{max(nf, 1)}] = {{{fs}}}; "
-                f"return spec::{fn}<W, {ne}, {nf}>(x, ev_, fs_, scratch + {vi_depth} * 64 * W, "
-                f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); }})()"), True
+        head = (f"([&]() -> int32_t {{ const int32_t ev_[{max(ne, 1)}] = {{{ev}}}; "
+                f"const int32_t fs_[{max(nf, 1)}] = {{{fs}}}; ")
+        lam = f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); }})()"
+        if eq_only:
+            return (head + f"return spec::exists_int_eq<W, {ne}, {nf}>(x, ev_, fs_, scratch + {vi_depth} * 64 * W, "
+                    + lam), True
+        # order comparisons: one candidate per breakpoint (exists_int_bp) instead of v-1, v, v+1
+        sh = _breakpoint_shifts(q, exprs, fsets)
+        return (head + f"const uint32_t sh_[{max(ne + nf, 1)}] = {{{', '.join(f'{m}u' for m in sh) or '0u'}}}; "
+                f"return spec::exists_int_bp<W, {ne}, {nf}>(x, ev_, fs_, sh_, scratch + {vi_depth} * 64 * W, "
+                + lam), True
 
 
 def _expensive(e) -> bool:
@@ -944,6 +950,36 @@ def _conjuncts(e):
     if isinstance(e, Bin) and e.op == "AND":
         return _conjuncts(e.x) + _conjuncts(e.y)
     return [e]
+
+
+# breakpoint offsets (bit d+1: b = e + d) of an atom `t OP e` with t the V.exists variable
+_BP_SHIFT = {"LE": 2, "GT": 2, "LT": 1, "GE": 1, "EQ": 3, "NE": 3}
+_FLIP = {"LE": "GE", "GE": "LE", "LT": "GT", "GT": "LT", "EQ": "EQ", "NE": "NE"}
+
+
+def _breakpoint_shifts(q, exprs, fsets):
+    """Per candidate source of _Compiler.witnesses (exprs, then field sets): the union of
+    the breakpoint offsets of the atoms comparing the variable with it (exists_int_bp)."""
+    uid = q.var.uid
+    es = [0] * len(exprs)
+    fm = {k: 0 for k in fsets}
+    for x in _walk(q.body):
+        if not (isinstance(x, Bin) and x.op in _BP_SHIFT):
+            continue
+        for a, b, op in ((x.x, x.y, x.op), (x.y, x.x, _FLIP[x.op])):
+            if not (isinstance(a, Var) and a.uid == uid):
+                continue
+            t = _strip(b)
+            if isinstance(t, Field):
+                fm[(t.f, t.tag)] |= _BP_SHIFT[op]
+            else:
+                hit = [i for i, e in enumerate(exprs) if e is t]
+                if not hit:
+                    return [7] * (len(exprs) + len(fsets))  # unmatched source: every offset (exact)
+                for i in hit:
+                    es[i] |= _BP_SHIFT[op]
+    out = es + [fm[k] for k in fsets]
+    return [m if m else 7 for m in out]
 
 
 def _eq_only(q) -> bool:

@@ -1,1 +1,1 @@
-bash scripts/gpu_ab_cfg.sh ab_lv2 "lv or lastvoting" C3_lastvoting,G1_lv_n64_fused,G1_otr_n64_fused libpsg_base libpsg
+bash scripts/gpu_ab_cfg.sh ab_spec1 "spec" G1_lv_n64_fused,G1_otr_n64_fused,G1_lv_n64_native libpsg

@@ -2,7 +2,7 @@
 
 Test infrastructure: an independent reading of the Formula semantics (no
 bytecode, no finitization: V.exists over Int is brute-forced over every value in
-[lo - 2, hi + 2] of the instance's trace plus Int.MinValue / Int.MaxValue), used
+[lo - 2, max(hi, R) + 2] of the instance's trace and rounds plus Int.MinValue / Int.MaxValue), used
 to check the compiler and both interpreters on specs the oracle has no
 hand-written counterpart for.
 """
@@ -23,13 +23,17 @@ class State:
         self.base = inst * self.per
         vals = [tr[self.base + k] for k in range(self.per)]
         vals = [v for v in vals if v != INT_MIN]
-        self.dom = list(range(min(vals + [0]) - 2, max(vals + [0]) + 3)) + [INT_MIN, INT_MAX]
+        # every trace value and every round number (terms like r / 4 + 1), +-2, and the extremes
+        self.dom = list(range(min(vals + [0]) - 2, max(vals + [0, R]) + 3)) + [INT_MIN, INT_MAX]
 
     def field(self, f, tag, p):
         if not (0 <= p < self.n):
             return 0
         cc = self.c if tag == F.TAG_CUR else (max(self.c - 1, 0) if tag == F.TAG_OLD else 0)
         return self.tr[self.base + (cc * 9 + f) * self.n + p]
+
+
+VINT_DOMAIN = None  # optional hook (quant, state, env) -> V.exists-over-Int domain (tests)
 
 
 def ev(e, st, env):
@@ -73,6 +77,8 @@ def ev(e, st, env):
         return ev(e.comp.body, st, env2)
     if isinstance(e, F.Quant):
         dom = range(st.n) if e.kind in ("forall", "exists", "count") else ((0, 1) if e.kind == "vbool" else st.dom)
+        if e.kind == "vint" and VINT_DOMAIN is not None:
+            dom = VINT_DOMAIN(e, st, env)
         res = []
         for v in dom:
             env2 = dict(env)

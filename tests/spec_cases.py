@@ -100,6 +100,21 @@ def pin_shapes():
     ])
 
 
+def order_shapes():
+    """V.exists over Int with order comparisons (the native lowering's breakpoint
+    finitization, spec::exists_int_bp: one candidate per breakpoint, not v-1, v, v+1)."""
+    return F.Spec(properties=[
+        ("OrdMajority", V.exists(lambda t: (P.filter(lambda i: i.x >= t).size > n // 2) & (t > r // 4))),
+        ("OrdBetween", V.exists(lambda t: (t > r) & (t < r + 2))),
+        ("OrdAbove", V.exists(lambda t: P.forall(lambda i: i.x < t) & (t <= 6 - r))),
+        ("OrdTop", V.exists(lambda t: P.forall(lambda i: i.x < t) & (t > r + 5))),
+        ("OrdNe", V.exists(lambda t: (t != r) & (t >= r) & (t <= r + 1))),
+        ("OrdMix", V.exists(lambda t: (t > 1) & P.exists(lambda i: i.x == t)
+                            & P.forall(lambda i: i.decided.implies(i.decision >= t)))),
+        ("OrdOld", V.exists(lambda t: P.forall(lambda i: old(i.x) <= t) & (t < r))),
+    ])
+
+
 # (id, algorithm, n, make_config kwargs, spec factory)
 CUSTOM = [
     ("fm-n12", psync.FloodMin(2), 12, dict(value_range=8, schedule=H(drop_log2=0, good_round=0.0, crash_fmax=3)),
@@ -126,4 +141,7 @@ CUSTOM = [
     ("fm-n8-pins", psync.FloodMin(2), 8, dict(value_range=3, schedule=H(drop_log2=0, good_round=0.0,
                                                                          crash_fmax=3)), pin_shapes),
     ("lv-n8-pins", psync.LastVoting(), 8, dict(value_range=3), pin_shapes),
+    ("otr-n16-order", psync.OTR(), 16, dict(value_range=3), order_shapes),
+    ("lv-n8-order", psync.LastVoting(), 8, dict(value_range=3, schedule=H(drop_log2=1, good_round=0.0)),
+     order_shapes),
 ]

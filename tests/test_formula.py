@@ -53,6 +53,37 @@ def test_custom_specs_match_direct_evaluation(cid, alg, n, kw, mk, oracle_mod):
     assert ff == rf and tm == rt
 
 
+def _breakpoint_domain(q, st, env):
+    """The native lowering's candidates for an order-compared V.exists (exists_int_bp):
+    each source's values shifted by its breakpoint offsets, plus Int.MaxValue."""
+    if F._eq_only(q):
+        return st.dom
+    exprs, fsets = F._Compiler().witnesses(q)
+    sh = F._breakpoint_shifts(q, exprs, fsets)
+    vals = [[formula_ref.ev(t, st, env)] for t in exprs]
+    vals += [[st.field(f, tag, p) for p in range(st.n)] for f, tag in fsets]
+    dom = {formula_ref.INT_MAX}
+    for vs, m in zip(vals, sh):
+        for v in vs:
+            dom |= {formula_ref._wrap(v + d) for d in (-1, 0, 1) if (m >> (d + 1)) & 1}
+    return sorted(dom)
+
+
+@pytest.mark.parametrize("cid,alg,n,kw,mk", [c for c in spec_cases.CUSTOM if c[2] <= 16] + [
+    ("lv-ref", psync.LastVoting(), 8, dict(value_range=3, schedule=H(drop_log2=1, good_round=0.0, crash_fmax=3)),
+     F.lv_spec)], ids=[c[0] for c in spec_cases.CUSTOM if c[2] <= 16] + ["lv-ref"])
+def test_breakpoint_finitization_is_exact(cid, alg, n, kw, mk, oracle_mod, monkeypatch):
+    """V.exists over Int decided on the breakpoint candidates (native exists_int_bp) equals
+    the brute-forced domain, check point by check point."""
+    cfg = psync.make_config(alg, n, seed=23, **kw)
+    spec = mk()
+    cnt = 8
+    tr = oracle_mod.trace(cfg, 0, cnt)
+    want = formula_ref.evaluate(spec, tr, cnt, n, cfg.rounds)
+    monkeypatch.setattr(formula_ref, "VINT_DOMAIN", _breakpoint_domain)
+    assert formula_ref.evaluate(spec, tr, cnt, n, cfg.rounds) == want
+
+
 def _rewritten(spec):
     """The Spec with every formula passed through the native lowering's V.exists rewrites."""
     memo = {}
