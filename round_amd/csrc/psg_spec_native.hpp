@@ -37,6 +37,10 @@ struct Ctx {
   // per check point: majority candidates already computed (key field | tag << 8, -1 = empty);
   // scalar slots, not an array, so they stay in registers
   int32_t maj_k0, maj_v0, maj_k1, maj_v1;
+  // member_init_own: per memo slot M, the lane's last probed value and its membership
+  // (valid once bit M of mok is set; a Ctx lives for one instance)
+  uint32_t mok = 0;
+  int32_t mv[4] = {0, 0, 0, 0}, mr[4] = {0, 0, 0, 0};
   PSG_DEV const int32_t* stage(int tag, int f) const { return sc + (tag * PSG_NFIELDS + f) * 64 * W; }
   PSG_DEV int32_t own(int tag, int f) const { return tag == PSG_TAG_CUR ? c[f] : (tag == PSG_TAG_OLD ? o[f] : i[f]); }
 };
@@ -191,6 +195,20 @@ PSG_DEV int32_t quant_tup_c(Ctx<W>& x, const TupU<NF>& tu, Fn fn, Fs... fs) {
 template <int W, int K>
 PSG_DEV int32_t member_init(Ctx<W>& x, int32_t t) {
   return (int32_t)x.iset[K].contains01(t);
+}
+
+// member_init of the lane's own current field F: the membership only changes with the
+// value, so each lane keeps its last probed value and answer (memo slot M) and the set
+// is probed again only when some lane's value changed (a group-uniform test)
+template <int W, int K, int F, int M>
+PSG_DEV int32_t member_init_own(Ctx<W>& x) {
+  const int32_t v = x.c[F];
+  if (!((x.mok >> M) & 1u) || x.g.any(v != x.mv[M])) {
+    x.mr[M] = (int32_t)x.iset[K].contains01(v);
+    x.mv[M] = v;
+    x.mok |= 1u << M;
+  }
+  return x.mr[M];
 }
 
 // ---------------------------------------------------------------- connectives with an expensive right side

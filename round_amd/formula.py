@@ -720,6 +720,7 @@ class _Gen:
         self.cse = {}         # id(closed subformula) -> C++ name of its hoisted value
         self.tup_sets = {}    # field tuple of a distinct-state quantifier -> C++ name of its per-check-point TupU
         self.tup_used = set()  # field tuples used by the function being generated
+        self.memo_slots = {}   # (init set, field) -> memo slot of member_init_own
 
     def gen(self, e, in_lane, vi_depth):
         """(C++ expression, depends on the lane)."""
@@ -798,8 +799,19 @@ class _Gen:
                     self.init_sets.append(f)
                 self.fields.add(f)
                 self.tags.add(TAG_INIT)
+                K = self.init_sets.index(f)
+                if (isinstance(t, Field) and t.tag == TAG_CUR and isinstance(t.proc, Var)
+                        and self.names.get(t.proc.uid, (None, False, False))[2]):
+                    # the lane's own current field: memoized probe (member_init_own)
+                    key = (K, t.f)
+                    if key not in self.memo_slots and len(self.memo_slots) < 4:
+                        self.memo_slots[key] = len(self.memo_slots)
+                    if key in self.memo_slots:
+                        self.fields.add(t.f)
+                        self.tags.add(TAG_CUR)
+                        return f"spec::member_init_own<W, {K}, {t.f}, {self.memo_slots[key]}>(x)", True
                 tc, tl = self.gen(t, in_lane, vi_depth)
-                return f"spec::member_init<W, {self.init_sets.index(f)}>(x, {tc})", tl
+                return f"spec::member_init<W, {K}>(x, {tc})", tl
             flds = _tuple_fields(q)
             if flds is not None:
                 # the body reads j only through fields: visit each distinct field tuple once
@@ -1216,15 +1228,23 @@ FUSED_KERNELS = {
 }
 
 
+FUSED_WPE = {abi.PSG_ALG_LAST_VOTING: 6}
+
+
 def _fused_source(alg: int, waves: Sequence[int]) -> str:
     """The algorithm's round kernel instantiated with the generated Spec as its hook:
     extern "C" psg_fused_a<alg>_w<W> (seeded HO sets) / psg_fused_x_a<alg>_w<W> (explicit)."""
+    import os
     src, body, targs = FUSED_KERNELS[alg]
     out = [f'#include "{src}"  // its kernel bodies; host launchers are compiled out (PSG_FUSED_MODULE)']
+    # occupancy target of the W = 1 kernels (0: the compiler's); LastVoting's generated check
+    # otherwise takes 92 VGPRs (5 waves/SIMD): 6 measured 155.6 -> 147.5 ms on C3 (7: no gain)
+    wpe = int(os.environ.get("PSG_FUSED_WPE", FUSED_WPE.get(alg, 0)))
     for W in waves:
         threads = 256 if W == 1 else 64 * W
+        attr = f"__attribute__((amdgpu_waves_per_eu({wpe}))) " if W == 1 and wpe > 0 else ""
         for suffix, xho in (("", "false"), ("x_", "true")):
-            out.append(f'extern "C" __global__ void __launch_bounds__({threads}) '
+            out.append(f'extern "C" __global__ void __launch_bounds__({threads}) {attr}'
                        f'psg_fused_{suffix}a{alg}_w{W}(psg::KArgs a) {{')
             out.append(f"  psg::{body}<{targs.format(W=W)}, {xho}, psg::spec::SpecHook<psg::GenSpec>>(a);")
             out.append("}")
