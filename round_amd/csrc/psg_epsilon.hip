@@ -66,6 +66,22 @@ PSG_DEV void wave_sort_key_pid(int64_t& key, int32_t& pid, int lane) {
   }
 }
 
+// 64 x 64 bit-matrix transpose across a wave: lane i holds row i; afterwards lane j holds
+// column j (bit i = bit j of row i). The six swap stages of the block transpose: at stage
+// s, the lane pair (i, i ^ s) exchanges the off-diagonal s x s blocks of its 2s x 2s block.
+PSG_DEV uint64_t wave_transpose64(uint64_t r, int lane) {
+  constexpr uint64_t kLo[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                               0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int st = 0; st < 6; ++st) {
+    const int s = 32 >> st;
+    const uint64_t lo = kLo[st], hi = ~kLo[st];
+    const uint64_t p = (uint64_t)__shfl_xor((unsigned long long)r, s);
+    r = (lane & s) ? ((r & hi) | ((p & hi) >> s)) : ((r & lo) | ((p & lo) << s));
+  }
+  return r;
+}
+
 // Slots: 0 EpsAgreement (no NaN decision, max - min <= eps), 1 EpsValidity (every
 // decision within [min, max] of the non-NaN initial values), 2 SafetyPredicate
 // (|V| >= n - f for every process that took a step). Termination: all decided.
@@ -183,17 +199,12 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a)
           // V), from the sorted pid column read at uniform positions. The selected members
           // j = f, 3f, 5f, ... < m - f are then found by dropping the lowest set bits, and
           // only those positions are read from LDS.
-          uint32_t us_lo = 0, us_hi = 0;
-          const int n_lo = n < 32 ? n : 32;
-          for (int t = 0; t < n_lo; ++t) {
-            const int q = __builtin_amdgcn_readlane(spid_r, t);
-            us_lo |= (uint32_t)((U.w[0] >> q) & 1ull) << t;
-          }
-          for (int t = 32; t < n; ++t) {
-            const int q = __builtin_amdgcn_readlane(spid_r, t);
-            us_hi |= (uint32_t)((U.w[0] >> q) & 1ull) << (t - 32);
-          }
-          const uint64_t Us = ((uint64_t)us_hi << 32) | us_lo;
+          // Us(p) bit t = [sorted position t's process is in U(p)]: transpose U (lane q: the
+          // receivers whose V holds q), fetch that column for position t's process, and
+          // transpose back (two bit-matrix transposes and one shuffle; padding processes
+          // sort last and are in no U)
+          const uint64_t Ut = wave_transpose64(U.w[0], g.lane);
+          const uint64_t Us = wave_transpose64((uint64_t)__shfl((unsigned long long)Ut, spid_r), g.lane);
           if (!halted && m > 0) {
             if (k == 0) {
               first = sx[__builtin_ctzll(Us)];
