@@ -278,6 +278,39 @@ PSG_DEV uint32_t gt01(int32_t a, int32_t b) { return (uint32_t)(((int64_t)b - (i
 
 // OR of a per-lane word over the wave (DPP row_shr 1/2/4/8, row_bcast 15/31),
 // returned as a uniform value (read from lane 63).
+// Lane l receives lane l ^ D's v, without the LDS crossbar: D = 1, 2 one DPP quad_perm;
+// D = 4, 8 a DPP row shift each way and a select; D = 16, 32 one v_permlane16/32_swap (a
+// half exchange of v with itself) and a select.
+// PSG_XSHFL_MASK: the distances D (bit log2 D) done in registers, the others by ds_bpermute.
+// Default none: on the VALU-bound Epsilon sort + transposes (W2 row) all-register measured
+// 18.1 ms, D = 16 / 32 only 16.1, D = 1 / 2 only 15.2, ds_bpermute for all 15.2 (the LDS
+// crossbar runs beside the VALU; the register forms cost 1-3 VALU per dword).
+#ifndef PSG_XSHFL_MASK
+#define PSG_XSHFL_MASK 0
+#endif
+template <int D>
+PSG_DEV uint32_t xshfl(uint32_t v, int lane) {
+  static_assert(D == 1 || D == 2 || D == 4 || D == 8 || D == 16 || D == 32, "xor distance");
+  if constexpr (((PSG_XSHFL_MASK >> __builtin_ctz(D)) & 1) == 0) return (uint32_t)__shfl_xor((int)v, D);
+  else if constexpr (D == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+  else if constexpr (D == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+  else if constexpr (D == 4 || D == 8) {
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + D, 0xF, 0xF, false);  // row_shl:D
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + D, 0xF, 0xF, false);  // row_shr:D
+    return (lane & D) ? dn : up;
+  } else if constexpr (D == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);  // odd rows <- even rows of v
+    return (lane & 16) ? (uint32_t)r[0] : (uint32_t)r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // upper half <- lower half of v
+    return (lane & 32) ? (uint32_t)r[0] : (uint32_t)r[1];
+  }
+}
+template <int D>
+PSG_DEV uint64_t xshfl64(uint64_t v, int lane) {
+  return (uint64_t)xshfl<D>((uint32_t)v, lane) | ((uint64_t)xshfl<D>((uint32_t)(v >> 32), lane) << 32);
+}
+
 PSG_DEV uint32_t wave_or(uint32_t v) {
   v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
   v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2

@@ -51,35 +51,37 @@ struct EpsLds {
 // Ascending bitonic sort of (key, pid) pairs over the 64 lanes of a wave (pairs must
 // be distinct; pids are). Stage (size, d): partners lane ^ d exchange through the LDS
 // crossbar; the lower lane of a pair keeps the smaller pair in an ascending block.
+template <int SIZE, int D>
+PSG_DEV void sort_stage(int64_t& key, int32_t& pid, int lane) {
+  const int64_t pk = (int64_t)xshfl64<D>((uint64_t)key, lane);
+  const int32_t pp = (int32_t)xshfl<D>((uint32_t)pid, lane);
+  const bool less = pk < key || (pk == key && pp < pid);  // partner's pair precedes mine
+  const bool take = less != (((lane & D) != 0) != ((lane & SIZE) != 0));
+  key = take ? pk : key;
+  pid = take ? pp : pid;
+  if constexpr (D > 1) sort_stage<SIZE, D / 2>(key, pid, lane);
+}
+template <int SIZE = 2>
 PSG_DEV void wave_sort_key_pid(int64_t& key, int32_t& pid, int lane) {
-#pragma unroll
-  for (int size = 2; size <= 64; size <<= 1) {
-#pragma unroll
-    for (int d = size >> 1; d > 0; d >>= 1) {
-      const int64_t pk = __shfl_xor(key, d);
-      const int32_t pp = __shfl_xor(pid, d);
-      const bool less = pk < key || (pk == key && pp < pid);  // partner's pair precedes mine
-      const bool take = less != (((lane & d) != 0) != ((lane & size) != 0));
-      key = take ? pk : key;
-      pid = take ? pp : pid;
-    }
-  }
+  sort_stage<SIZE, SIZE / 2>(key, pid, lane);  // partners exchange in registers (xshfl)
+  if constexpr (SIZE < 64) wave_sort_key_pid<SIZE * 2>(key, pid, lane);
 }
 
 // 64 x 64 bit-matrix transpose across a wave: lane i holds row i; afterwards lane j holds
 // column j (bit i = bit j of row i). The six swap stages of the block transpose: at stage
 // s, the lane pair (i, i ^ s) exchanges the off-diagonal s x s blocks of its 2s x 2s block.
+template <int S, uint64_t LO>
+PSG_DEV uint64_t transpose_stage(uint64_t r, int lane) {
+  const uint64_t p = xshfl64<S>(r, lane);
+  return (lane & S) ? ((r & ~LO) | ((p & ~LO) >> S)) : ((r & LO) | ((p & LO) << S));
+}
 PSG_DEV uint64_t wave_transpose64(uint64_t r, int lane) {
-  constexpr uint64_t kLo[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
-                               0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
-#pragma unroll
-  for (int st = 0; st < 6; ++st) {
-    const int s = 32 >> st;
-    const uint64_t lo = kLo[st], hi = ~kLo[st];
-    const uint64_t p = (uint64_t)__shfl_xor((unsigned long long)r, s);
-    r = (lane & s) ? ((r & hi) | ((p & hi) >> s)) : ((r & lo) | ((p & lo) << s));
-  }
-  return r;
+  r = transpose_stage<32, 0x00000000FFFFFFFFull>(r, lane);
+  r = transpose_stage<16, 0x0000FFFF0000FFFFull>(r, lane);
+  r = transpose_stage<8, 0x00FF00FF00FF00FFull>(r, lane);
+  r = transpose_stage<4, 0x0F0F0F0F0F0F0F0Full>(r, lane);
+  r = transpose_stage<2, 0x3333333333333333ull>(r, lane);
+  return transpose_stage<1, 0x5555555555555555ull>(r, lane);
 }
 
 // Slots: 0 EpsAgreement (no NaN decision, max - min <= eps), 1 EpsValidity (every
