@@ -270,7 +270,7 @@ def main():
             rl["traffic_unit"] = "GB/s"
             rl["traffic_bytes_per_launch"] = d["hbm"]["traffic_bytes"]
             rl["traffic_source"] = src + " (PMC FETCH_SIZE*2 + WRITE_SIZE per launch)"
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the host baseline is an N = 1 figure
             out["cpu_baseline"] = cpu_baseline(head["cfg"], args.cpu_seconds)
         else:
             out["cpu_baseline"] = None

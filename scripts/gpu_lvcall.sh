@@ -1,1 +1,1 @@
-bash scripts/gpu_ab_cfg.sh ab_eps1 "eps" W2_epsilon libpsg_base libpsg
+bash scripts/gpu_ab.sh ab_lvk C3_lastvoting libpsg libpsg_k1 libpsg_k2
