@@ -7,6 +7,8 @@
 // maxBy over the R0 mailbox (LastVoting.scala:132) takes the first max in Scala
 // Map iteration order: insertion order (ascending pid) up to 4 entries, CHAMP
 // order beyond, computed from per-lane CHAMP sort keys and a wave min-reduction.
+#include <type_traits>
+
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
 
@@ -221,7 +223,9 @@ PSG_DEV void lv_body(const KArgs& a) {
     if (tracing<SH>(a)) trace(0, n);
     pt.mark(0);
 
-    for (int k = 0; k < a.R; ++k) {
+    // one round of slot RS = k mod 4 (compile time: each slot's step and check specialized)
+    auto round = [&](const int k, auto RSc) {
+      constexpr int RS = decltype(RSc)::value;
       const uint32_t old_fl = fl;
       const int32_t old_decision = decision;
       const Mask<W> act = g.ballot((fl & F_HALTED) == 0u);
@@ -237,10 +241,10 @@ PSG_DEV void lv_body(const KArgs& a) {
         if (sc.crash_on) cs.sets(g, k, CB, CN);
         // R1 / R3 read bit coord of every HO(p) (a mailbox of at most the coordinator's
         // message); R0 / R2 only HO(coord)
-        const bool coordRound = (k & 1) == 0;
+        constexpr bool coordRound = (RS & 1) == 0;
         // R1 / R3: does the coordinator send (commit / ready, LastVoting.scala:141, 187)? When it
         // does not, no mailbox is read and no HO bit of the round is observed
-        const bool sent = !coordRound && cAlive && mtest(g.ballot((fl & ((k & 3) == 1 ? F_COMMIT : F_READY)) != 0u), c);
+        const bool sent = !coordRound && cAlive && mtest(g.ballot((fl & (RS == 1 ? F_COMMIT : F_READY)) != 0u), c);
         Mask<W> HO = mzero<W>(), HOc = mzero<W>();
         if constexpr (XHO) {
           HO = sc.ho(k, g.pid, good, goodS, CB, CN);
@@ -253,68 +257,65 @@ PSG_DEV void lv_body(const KArgs& a) {
           sc.draw((uint32_t)k, (uint32_t)g.pid, good, crash, dm, hf);
           HO = sc.assemble(g.pid, good, goodS, CB, CN, dm, hf);
         }
-        if (coordRound) {
+        if constexpr (coordRound) {
           if constexpr (XHO) HOc = ho_of<W>(g, L, HO, c);
           else HOc = cw.ho(sc, k, c, g.lane, n, good, goodS, CB, CN);
         }
         pt.mark(1);
         lv_stage<W>(g, L, x, ts, vote, decision);
-        switch (k & 3) {
-          case 0: {  // R0: send (x, ts) to coord; coord picks vote = x of maxBy ts
-            const Mask<W> Mc = mand(HOc, act);
-            const int size = mpopc(Mc);
-            hs = g.pid == c ? size : 0;
-            if (cAlive && (size > n / 2 || (k == 0 && size > 0))) {
-              const int32_t v = maxby_ts_x<W>(g, L.xs, Mc, size, x, ts, myh, a.tiebreak);
-              if (g.pid == c) {
-                vote = v;
-                fl |= F_COMMIT;
-              }
+        if constexpr (RS == 0) {  // R0: send (x, ts) to coord; coord picks vote = x of maxBy ts
+          const Mask<W> Mc = mand(HOc, act);
+          const int size = mpopc(Mc);
+          hs = g.pid == c ? size : 0;
+          if (cAlive && (size > n / 2 || (k == 0 && size > 0))) {
+            const int32_t v = maxby_ts_x<W>(g, L.xs, Mc, size, x, ts, myh, a.tiebreak);
+            if (g.pid == c) {
+              vote = v;
+              fl |= F_COMMIT;
             }
-            break;
           }
-          case 1: {  // R1: coord broadcasts vote if commit; receivers adopt (x, ts = r/4)
-            hs = sent && mtest(HO, c) ? 1 : 0;
-            if (sent) {
-              const int32_t vc = g.bcast(vote, L.votes, c);
-              const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
-              const uint32_t vin = SH::kFused ? 1u : X0.contains01(vc);  // one probe of a uniform value
-              x = rcv ? vc : x;
-              xin = rcv ? vin : xin;
-              ts = rcv ? phase : ts;
-            }
-            break;
+        } else if constexpr (RS == 1) {  // R1: coord broadcasts vote if commit; receivers adopt (x, ts = r/4)
+          hs = sent && mtest(HO, c) ? 1 : 0;
+          if (sent) {
+            const int32_t vc = g.bcast(vote, L.votes, c);
+            const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
+            const uint32_t vin = SH::kFused ? 1u : X0.contains01(vc);  // one probe of a uniform value
+            x = rcv ? vc : x;
+            xin = rcv ? vin : xin;
+            ts = rcv ? phase : ts;
           }
-          case 2: {  // R2: ts == r/4 send x to coord; coord ready on a majority
-            const Mask<W> Mc = mand(mand(HOc, act), g.ballot(ts == phase));
-            hs = g.pid == c ? mpopc(Mc) : 0;
-            if (cAlive && mpopc(Mc) > need2 && g.pid == c) fl |= F_READY;
-            break;
+        } else if constexpr (RS == 2) {  // R2: ts == r/4 send x to coord; coord ready on a majority
+          const Mask<W> Mc = mand(mand(HOc, act), g.ballot(ts == phase));
+          hs = g.pid == c ? mpopc(Mc) : 0;
+          if (cAlive && mpopc(Mc) > need2 && g.pid == c) fl |= F_READY;
+        } else {  // R3: coord broadcasts vote if ready; receivers decide and exit
+          hs = sent && mtest(HO, c) ? 1 : 0;
+          if (sent) {
+            const int32_t vc = g.bcast(vote, L.votes, c);
+            const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
+            const uint32_t vin = SH::kFused ? 1u : X0.contains01(vc);
+            din = rcv ? vin : din;
+            const uint32_t first = rcv & (dec_round < 0 ? 1u : 0u);
+            dec_val = first ? vc : dec_val;
+            dec_round = first ? k : dec_round;
+            decision = rcv ? vc : decision;
+            halt_round = rcv ? k : halt_round;
+            fl |= rcv ? (F_DECIDED | F_HALTED) : 0u;
           }
-          default: {  // R3: coord broadcasts vote if ready; receivers decide and exit
-            hs = sent && mtest(HO, c) ? 1 : 0;
-            if (sent) {
-              const int32_t vc = g.bcast(vote, L.votes, c);
-              const uint32_t rcv = live & (mtest(HO, c) ? 1u : 0u);
-              const uint32_t vin = SH::kFused ? 1u : X0.contains01(vc);
-              din = rcv ? vin : din;
-              const uint32_t first = rcv & (dec_round < 0 ? 1u : 0u);
-              dec_val = first ? vc : dec_val;
-              dec_round = first ? k : dec_round;
-              decision = rcv ? vc : decision;
-              halt_round = rcv ? k : halt_round;
-              fl |= rcv ? (F_DECIDED | F_HALTED) : 0u;
-            }
-            // ready = false; commit = false for every process that took this step
-            fl &= live ? ~(F_READY | F_COMMIT) : ~0u;
-            break;
-          }
+          // ready = false; commit = false for every process that took this step
+          fl &= live ? ~(F_READY | F_COMMIT) : ~0u;
         }
         pt.mark(2);
       }
       if constexpr (!SH::kFused) lv_check<W>(g, L, ck, k + 1, true, n, full, x, ts, vote, decision, fl, old_fl, old_decision, xin, din);
       if (tracing<SH>(a)) trace(k + 1, (old_fl & F_HALTED) ? n : hs);
       pt.mark(many(act) ? 4 : 5);
+    };
+    for (int k0 = 0; k0 < a.R; k0 += 4) {
+      round(k0, std::integral_constant<int, 0>{});
+      if (k0 + 1 < a.R) round(k0 + 1, std::integral_constant<int, 1>{});
+      if (k0 + 2 < a.R) round(k0 + 2, std::integral_constant<int, 2>{});
+      if (k0 + 3 < a.R) round(k0 + 3, std::integral_constant<int, 3>{});
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 7, dec_val, dec_round, halt_round, x, &bc);
     pt.mark(3);

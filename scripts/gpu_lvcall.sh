@@ -1,1 +1,1 @@
-bash scripts/gpu_ab.sh ab_lvk C3_lastvoting libpsg libpsg_k1 libpsg_k2
+bash scripts/gpu_ab_cfg.sh ab_lvs2 "lv or lastvoting" C3_lastvoting,G1_lv_n64_fused libpsg
