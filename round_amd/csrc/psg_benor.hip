@@ -6,6 +6,8 @@
 // `util.Random.nextBoolean` (BenOr.scala:77) is java.util.Random's first
 // nextBoolean after setSeed(Philox(seed, instance, round, pid)).
 // n = 128 runs as W = 2 waves per instance with the ballot words exchanged in LDS.
+#include <type_traits>
+
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
 #include "psg_packed.hpp"
@@ -228,8 +230,10 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
   Checks ck;
   ck.reset();
   Mask<W> act, T1, T2;  // the next round's alive set and payload masks
-  auto check = [&](int c, bool has_old) {
-    const bool r0next = (c & 1) == 0;  // round c is an R0
+  // check point c (parity CP = c & 1 at compile time: round c is an R0 iff CP == 0)
+  auto check = [&](int c, bool has_old, auto CPc) {
+    constexpr int CP = decltype(CPc)::value;
+    constexpr bool r0next = CP == 0;
     uint32_t fw = 0;                   // bit b: the Spec witness b holds for some process of the lane
     uint32_t al[W], t1[W], t2[W], xs[W], ds[W];
 #pragma unroll
@@ -261,15 +265,17 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
     const int cntF = n - cntT;
     const bool noDec = !(flags & 1u);
     const bool ex = (cntF > n / 2 && !(flags & 2u)) || (cntT > n / 2 && !(flags & 4u));
-    const bool rfail = (c & 1) != 0 && ((!(cntT > n / 2) && (flags & 32u)) || (!(cntF > n / 2) && (flags & 64u)));
+    const bool rfail = CP != 0 && ((!(cntT > n / 2) && (flags & 32u)) || (!(cntF > n / 2) && (flags & 64u)));
     const bool inv0 = (noDec || ex) && !rfail;
     const bool same = !((flags & 8u) && (flags & 16u));
     const bool irrev = !(flags & 128u);
     const bool pred = !(flags & 256u);
     ck.record(fbit(inv0, 0) | fbit(inv0, 1) | fbit(same, 2) | fbit(irrev, 3) | fbit(pred, 4), cntD == n, c, P.lane);
   };
-  check(0, false);
-  for (int k = 0; k < a.R; ++k) {
+  check(0, false, std::integral_constant<int, 0>{});
+  // one round of slot RS = k & 1 (compile time: the R0 / R1 step and the next check specialized)
+  auto round = [&](const int k, auto RSc) {
+    constexpr int RS = decltype(RSc)::value;
 #pragma unroll
     for (int j = 0; j < W; ++j) {
       old_decided[j] = decided[j];
@@ -287,7 +293,7 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
           CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
         }
       }
-      const bool even = (k & 1) == 0;
+      constexpr bool even = RS == 0;
       const Mask<W> A1 = mand(T1, act), A2 = mand(T2, act);  // R0: x / canDecide; R1: vote true / false
 #pragma unroll
       for (int j = 0; j < W; ++j) {
@@ -295,7 +301,7 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
         const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
         const int size = mpopc(M);
         predw[j] = P.val[j] & (size <= n / 2 ? 1u : 0u);
-        if (even) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
+        if constexpr (even) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
           if (cd[j]) {
             dec_val[j] = (int32_t)x[j];
             dec_round[j] = k;
@@ -331,7 +337,11 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
         if (halt_round[j] == k) halted[j] = 1;
       }
     }
-    check(k + 1, true);
+    check(k + 1, true, std::integral_constant<int, (RS + 1) & 1>{});
+  };
+  for (int k0 = 0; k0 < a.R; k0 += 2) {
+    round(k0, std::integral_constant<int, 0>{});
+    if (k0 + 1 < a.R) round(k0 + 1, std::integral_constant<int, 1>{});
   }
   int32_t fx[W];
 #pragma unroll
@@ -339,8 +349,11 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
   pk_finish<W>(P, a, i, ck, 5, dec_val, dec_round, halt_round, fx, bc);
 }
 
+#ifndef PSG_BO_PK_WPE
+#define PSG_BO_PK_WPE 4  // parity-specialized loop: 4 waves/SIMD (no scratch) 37.9 ms vs 5: 38.4 (C5)
+#endif
 template <int W>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_PK_WPE))) benor_packed_kernel(KArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_BO_PK_WPE))) benor_packed_kernel(KArgs a) {
   __shared__ BlockCounters bc;
   counters_init(&bc);
   __syncthreads();
