@@ -19,6 +19,8 @@
 // Map order by psg_selftest_map_head.
 // Spec: TrivialSpec; the build checks uniform agreement (k = 1 over every
 // decider, HO-model consensus) and validity.
+#include <type_traits>
+
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
 
@@ -105,7 +107,9 @@ PSG_DEV void slv_body(const KArgs& a) {
     };
     if (tracing<SH>(a)) trace(0, n);
 
-    for (int k = 0; k < a.R; ++k) {
+    // one round of slot RS = k mod 3 (compile time: each slot's step specialized)
+    auto round = [&](const int k, auto RSc) {
+      constexpr int RS = decltype(RSc)::value;
       const Mask<W> act = g.ballot((fl & S_HALTED) == 0u);
       const uint32_t fl_start = fl;
       int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
@@ -118,14 +122,17 @@ PSG_DEV void slv_body(const KArgs& a) {
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) cs.sets(g, k, CB, CN);
-        const Mask<W> HO = sc.ho(k, g.pid, good, goodS, CB, CN);
+        // R1 reads only bit coord of HO(p), and only when the coordinator sends
+        // (ShortLastVoting.scala:53): the other rounds' and silent R1s' draws are skipped
+        const bool sent = RS == 1 && cAlive && mtest(g.ballot((fl & S_COMMIT) != 0u), c);
+        Mask<W> HO = mzero<W>();
+        if (RS != 1 || sent) HO = sc.ho(k, g.pid, good, goodS, CB, CN);
         if constexpr (W > 1) {
           L.xs[g.pid] = x;
           L.votes[g.pid] = vote;
           __syncthreads();
         }
-        const int m3 = k % 3;
-        if (m3 == 0) {  // R0 (ShortLastVoting.scala:34-47)
+        if constexpr (RS == 0) {  // R0 (ShortLastVoting.scala:34-47)
           const Mask<W> Mc = mand(slv_ho_of<W>(g, L, HO, c), act);
           const int size = mpopc(Mc);
           hs = g.pid == c ? size : 0;
@@ -136,8 +143,7 @@ PSG_DEV void slv_body(const KArgs& a) {
               fl |= S_COMMIT;
             }
           }
-        } else if (m3 == 1) {  // R1 (ShortLastVoting.scala:51-69)
-          const bool sent = cAlive && mtest(g.ballot((fl & S_COMMIT) != 0u), c);
+        } else if constexpr (RS == 1) {  // R1 (ShortLastVoting.scala:51-69)
           hs = sent && mtest(HO, c) ? 1 : 0;
           if (sent) {
             const int32_t vc = g.bcast(vote, L.votes, c);
@@ -176,6 +182,11 @@ PSG_DEV void slv_body(const KArgs& a) {
       }
       if constexpr (!SH::kFused) check(k + 1);
       if (tracing<SH>(a)) trace(k + 1, (fl_start & S_HALTED) ? n : hs);
+    };
+    for (int k0 = 0; k0 < a.R; k0 += 3) {
+      round(k0, std::integral_constant<int, 0>{});
+      if (k0 + 1 < a.R) round(k0 + 1, std::integral_constant<int, 1>{});
+      if (k0 + 2 < a.R) round(k0 + 2, std::integral_constant<int, 2>{});
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 2, dec_val, dec_round, halt_round, x, &bc);
   }
@@ -183,8 +194,12 @@ PSG_DEV void slv_body(const KArgs& a) {
   counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 2, a.R);
 }
 
+#ifndef PSG_SLV_WPE
+#define PSG_SLV_WPE 7  // W = 1 occupancy target: 7 measured 65.2 ms vs 6: 66.0, compiler (5): 70.5 (W2 row)
+#endif
 template <int W, bool XHO, class SH = NoHook>
-__global__ void __launch_bounds__(Geometry<W>::kThreads) slv_kernel(KArgs a) {
+__global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? PSG_SLV_WPE : 1)))
+slv_kernel(KArgs a) {
   slv_body<W, XHO, SH>(a);
 }
 

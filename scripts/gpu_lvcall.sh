@@ -1,1 +1,1 @@
-bash scripts/gpu_ab_cfg.sh ab_lvs2 "lv or lastvoting" C3_lastvoting,G1_lv_n64_fused libpsg
+bash scripts/gpu_ab.sh ab_slv2 W2_slv libpsg libpsg_w6 libpsg_w7
