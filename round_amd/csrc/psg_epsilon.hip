@@ -101,8 +101,12 @@ PSG_DEV void eps_check(Grp<W>& g, Checks& ck, int c, const Mask<W>& full, bool d
   ck.record(fbit(agree, 0) | fbit(valid, 1) | fbit(pred, 2), meq(g.ballot(decided), full), c, g.lane);
 }
 
+#ifndef PSG_EPS_WPE
+#define PSG_EPS_WPE 7  // W = 1 occupancy target: 7 measured 14.2 ms vs 6: 14.4, compiler (5): 15.3 (W2 row)
+#endif
 template <int W, bool XHO>
-__global__ void __launch_bounds__(Geometry<W>::kThreads) epsilon_kernel(KArgs a) {
+__global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? PSG_EPS_WPE : 1)))
+epsilon_kernel(KArgs a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int32_t crl[W > 1 ? 64 * W : 1];
