@@ -176,26 +176,28 @@ PSG_DEV void otr_body(const KArgs& a) {
             __syncthreads();
           }
           uint64_t best = (uint64_t)(uint32_t)(INT32_MAX ^ 0x7FFFFFFF);  // count 0, v = INT32_MAX
-          Mask<W> pass1 = act;  // the values folded by the first pass
-          bool two = false;
+          Mask<W> rem = act, passB = mzero<W>(), passS = mzero<W>();
+          int stage = 2;  // 2: a single pass over every value
           if constexpr (W == 1) {
-            // Round 0 with many distinct values (V = 64: ~40): values held by one alive sender
-            // count at most 1 in any mailbox, so they can win (or tie) only where no value
-            // counts 2. Count each value's alive holders in LDS (the X0 table is free in
-            // bitmap mode: every x is an initial value, x - lo < 64), fold the multiply-held
-            // values first and the singly-held ones only if some updating lane's best count
-            // is still < 2. V = 64: 33.45 -> 30.7 ms; with few distinct initial values the
-            // single pass is already short and the counting is skipped.
+            // Round 0 with many distinct values (V = 64: ~40 of 64): a value held by h alive
+            // senders counts at most h in any mailbox, so values are folded by decreasing
+            // holder classes — h >= 3, then h = 2, then h = 1 — and a class is skipped when
+            // every updating lane's best count already exceeds its h (it can neither win
+            // nor tie). Holders are counted in LDS (the X0 table is free in bitmap mode:
+            // every x is an initial value, x - lo < 64). With few distinct initial values
+            // the single pass is already short and the counting is skipped.
             if (k == 0 && X0.bmode && __builtin_popcountll(X0.bm) > 8) {
               int32_t* cnt = x0tab[grp];
               cnt[g.lane] = 0;
               const uint32_t slot = (uint32_t)(x - X0.lo) & 63u;
               if (!halted01) atomicAdd(&cnt[slot], 1);
-              pass1 = mand(act, g.ballot_any(cnt[slot] >= 2));  // every holder of such a value
-              two = true;
+              const int32_t h = cnt[slot];
+              rem = mand(act, g.ballot_any(h >= 3));  // every holder of such a value
+              passB = mand(act, g.ballot_any(h == 2));
+              passS = mandn(act, mor(rem, passB));
+              stage = 0;
             }
           }
-          Mask<W> rem = pass1;
           while (true) {
             while (many(rem)) {
               const int32_t kv = g.bcast(xv, L.xs, mfirst(rem));
@@ -204,9 +206,11 @@ PSG_DEV void otr_body(const KArgs& a) {
               const uint64_t key = ((uint64_t)(uint32_t)mpopc(mand(M, E)) << 32) | (uint32_t)kv;
               best = key > best ? key : best;
             }
-            if (!two || !g.any(upd != 0u && (uint32_t)(best >> 32) < 2u)) break;
-            rem = mandn(act, pass1);  // the singly-held values
-            two = false;
+            if (stage == 2) break;
+            const uint32_t beat = stage == 0 ? 3u : 2u;  // the next class's values count < beat
+            if (!g.any(upd != 0u && (uint32_t)(best >> 32) < beat)) break;
+            rem = stage == 0 ? passB : passS;
+            ++stage;
           }
           const int32_t best_c = (int32_t)(best >> 32);
           const int32_t best_v = (int32_t)((uint32_t)best ^ 0x7FFFFFFFu);
