@@ -46,34 +46,39 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
     L.ds[g.pid] = decision;
     __syncthreads();
   }
+  uint32_t od, ox;
+  X0.maybe_out01_2(decision, x, od, ox);
+  const uint32_t irr01 = has_old ? old01 & (1u - (dec01 & eq01(old_decision, decision))) : 0u;
+  {
+    // Settled state first (every process decided, every decision equal to process 0's, no
+    // witness): one ballot of a per-process word, with process 0's decision as d0 (when all
+    // decided, process 0 is the first decider). Then keepInit, Validity, Agreement and
+    // Irrevocability hold, so Invariant2 (OTR: term && all decisions equal and initial;
+    // OTR2: all decisions equal), Safety and Integrity hold; Invariant0 reduces to e0
+    // (OTR2: term), Invariant1 to e1, with the vote count taken at v = d0. The same values
+    // as the general path below, in a few instructions (most check points of a run are in
+    // this state).
+    const int32_t p0 = g.bcast(decision, L.ds, 0);
+    uint32_t u = (1u - dec01) | od | ne01(decision, p0) | irr01;
+    if constexpr (!V2) u |= ox;  // keepInit (OTR only)
+    if (!g.any((u & valid01) != 0u)) {
+      const int cnt = mpopc(g.ballot_any((valid01 & eq01(x, p0)) != 0u));
+      const uint32_t fb = (V2 ? 0u : fbit(cnt > sthr, 1)) | fbit(cnt == n, 2);
+      ck.record(fb, true, c, g.lane);
+      return;
+    }
+  }
   // dec01 and the witness word are 0 on lanes past n: ballots without the valid-lane mask
   const Mask<W> D = g.ballot_any(dec01 != 0u);
   const bool anyD = many(D);
   const int32_t d0 = anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
-  uint32_t od, ox;
-  X0.maybe_out01_2(decision, x, od, ox);
   uint32_t wit = od | ne01(decision, d0);
   if constexpr (!V2) wit = (wit & dec01) | ox;  // keepInit (OTR only)
   else wit &= dec01;
-  if (has_old) wit |= old01 & (1u - (dec01 & eq01(old_decision, decision)));
+  wit |= irr01;
   const Mask<W> Wm = g.ballot_any((wit & valid01) != 0u);
-  uint64_t unsettled = 0;  // some process undecided, or some possible witness
-#pragma unroll
-  for (int w = 0; w < W; ++w) unsettled |= (D.w[w] ^ full.w[w]) | Wm.w[w];
   const bool term = meq(D, full);
   const bool wany = many(Wm);
-  if (unsettled == 0) {
-    // Settled state (every process decided, no witness): keepInit, Validity, Agreement
-    // and Irrevocability hold, so Invariant2 (OTR: term && all decisions equal and
-    // initial; OTR2: all decisions equal), Safety and Integrity hold; Invariant0 reduces
-    // to e0 (OTR2: term), Invariant1 to e1, with the vote count taken at v = d0. The
-    // same values as the general path below, in a few scalar instructions (most check
-    // points of a run are in this state).
-    const int cnt = mpopc(g.ballot_any((valid01 & eq01(x, d0)) != 0u));
-    const uint32_t fb = (V2 ? 0u : fbit(cnt > sthr, 1)) | fbit(cnt == n, 2);
-    ck.record(fb, true, c, g.lane);
-    return;
-  }
   bool keep = true, validity = true, same = true, irrev = true;
   if (wany) {  // exact resolution, one ballot per formula
     if constexpr (!V2) keep = X0.all_in(g, full, x);
