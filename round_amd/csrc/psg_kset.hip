@@ -41,22 +41,24 @@ PSG_DEV int32_t kset_pick(const Mask<W>& t, const int32_t* x0s, const Mask<W>& E
   return m;
 }
 
-template <int W>
+// t mask of process q from the staged rows: [pid][word] (CS = 0) or [word][pid] with a
+// column stride CS (the lane-packed path: lanes store consecutive words, no bank conflicts)
+template <int W, int CS = 0>
 PSG_DEV Mask<W> load_t(const uint64_t* ts, int q) {
   Mask<W> m;
 #pragma unroll
-  for (int w = 0; w < W; ++w) m.w[w] = ts[q * W + w];
+  for (int w = 0; w < W; ++w) m.w[w] = CS ? ts[w * CS + q] : ts[q * W + w];
   return m;
 }
 
 // `content.find(_._1)` of receiver p (KSetAgreement.scala:53): the first decider message in
 // Scala Map iteration order — the first pid of cand up to 4 mailbox entries (Map1..Map4)
 // or when the candidates agree on t; otherwise the CHAMP order's first (min sort key).
-template <int W>
+template <int W, int CS = 0>
 PSG_DEV int kset_find(const KArgs& a, const uint64_t* ts, const Mask<W>& M, const Mask<W>& cand) {
   int qs = mfirst(cand);
   if (a.tiebreak == PSG_TIE_CHAMP && mpopc(M) > 4 && mpopc(cand) > 1) {
-    const Mask<W> t0 = load_t<W>(ts, qs);
+    const Mask<W> t0 = load_t<W, CS>(ts, qs);
     bool differ = false;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
@@ -64,7 +66,7 @@ PSG_DEV int kset_find(const KArgs& a, const uint64_t* ts, const Mask<W>& M, cons
       while (m) {
         const int q = w * 64 + __builtin_ctzll(m);
         m &= m - 1;
-        if (!meq(load_t<W>(ts, q), t0)) differ = true;
+        if (!meq(load_t<W, CS>(ts, q), t0)) differ = true;
       }
     }
     if (differ) {
@@ -100,8 +102,10 @@ PSG_DEV int kset_find(const KArgs& a, const uint64_t* ts, const Mask<W>& M, cons
 
 // ---------------------------------------------------------------- lane-packed path (n > 64)
 // kset_body's built-in-checker path with one wave per instance and the W processes
-// l + 64 j in lane l (psg_packed.hpp): the t masks are staged in this wave's LDS (one
-// 8 W-byte row per process) for the uniform class reads and the per-lane find; the
+// l + 64 j in lane l (psg_packed.hpp): the t masks are staged in this wave's LDS (word-major,
+// [word][pid]: each store instruction writes 64 consecutive words, no bank conflicts; the
+// pid-major rows measured 47 % of LDS cycles in conflicts) for the uniform class reads and
+// the per-lane find; the
 // k-agreement check's ballots are wave ballots; no round needs a block barrier.
 template <int W>
 struct KsPk {
@@ -171,7 +175,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
 #pragma unroll
       for (int j = 0; j < W; ++j)
 #pragma unroll
-        for (int w = 0; w < W; ++w) L.ts[P.pid(j) * W + w] = t[j].w[w];
+        for (int w = 0; w < W; ++w) L.ts[w * 64 * W + P.pid(j)] = t[j].w[w];  // [word][pid]
       lds_sync<1>();
       // round 0 (every alive sender still holds only its own origin): closed form below
       uint32_t notown[W];
@@ -207,7 +211,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
             rem = mzero<W>();
           }
           for (int cls = 0; cls < kClasses && many(rem); ++cls) {
-            const Mask<W> tq = load_t<W>(L.ts, mfirst(rem));
+            const Mask<W> tq = load_t<W, 64 * W>(L.ts, mfirst(rem));
             uint32_t mine[W];
 #pragma unroll
             for (int jj = 0; jj < W; ++jj) mine[jj] = meq(t[jj], tq) ? 1u : 0u;
@@ -219,7 +223,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
           }
           while (many(rem)) {
             const int q = mtake_first(rem);
-            const Mask<W> tq = load_t<W>(L.ts, q);
+            const Mask<W> tq = load_t<W, 64 * W>(L.ts, q);
             if (mtest(M, q)) {
               same += meq(tq, t[j]) ? 1 : 0;
               uni = mor(uni, tq);
@@ -231,7 +235,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
           }
         }
         if (adopt) {  // t = content.find(_._1).get._2 — first decider message in iteration order
-          tnew[j] = load_t<W>(L.ts, kset_find<W>(a, L.ts, M, mand(M, Dm)));
+          tnew[j] = load_t<W, 64 * W>(L.ts, kset_find<W, 64 * W>(a, L.ts, M, mand(M, Dm)));
           becomeDec[j] = 1;
         }
         if (!halted[j] && decider[j]) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:48-50)
