@@ -158,6 +158,49 @@ def test_host_supplied_inputs(oracle_mod):
     assert [_inst_tuple(s) for s in res.per_instance] == [_inst_tuple(s) for s in opi]
 
 
+@pytest.mark.parametrize("drop", [3, 5])
+@pytest.mark.parametrize("alg", [psync.OTR(), psync.OTR2()], ids=["otr", "otr2"])
+@pytest.mark.parametrize("n", [64, 40, 9])
+def test_otr_round0_value_classes(alg, n, drop, oracle_mod):
+    """Round 0's mmor folds values by holder classes (h >= 3, h = 2, h = 1) when the initial
+    values fit the X0 bitmap and more than 8 are distinct: inputs where every value is held
+    once (the singleton pass must run), twice, mixed with ties across classes, values at the
+    edges of the 64-wide bitmap window (negative too), and spread-out values (hash mode, one
+    pass), with links lost w.p. 1/8 and 1/32 (mailboxes above the 2n/3 quorum), against the
+    oracle; the test also requires that round 0 updated x in most instances."""
+    import random
+    rng = random.Random(1000 + n)
+    count = 240
+    init = []
+    for i in range(count):
+        fam = i % 6
+        if fam == 0:    # all distinct (n <= 64): only singletons
+            row = rng.sample(range(1, 65), n)
+        elif fam == 1:  # every value held twice
+            row = [1 + (p // 2) for p in range(n)]
+            rng.shuffle(row)
+        elif fam == 2:  # mixed classes with ties
+            row = [rng.choice([3, 3, 3, 7, 7, 11, 11]) if p % 3 == 0 else rng.randint(1, 64) for p in range(n)]
+        elif fam == 3:  # the whole 64-wide window, negative base
+            row = [-1000 + rng.randint(0, 63) for _ in range(n)]
+            row[0], row[-1] = -1000, -937
+        elif fam == 4:  # hash mode: values spread over more than 64
+            row = [rng.randint(0, 40) * 1000 for _ in range(n)]
+        else:           # near Int.MaxValue, within one window
+            row = [2147483647 - rng.randint(0, 63) for _ in range(n)]
+        init.append(row)
+    sched = H(drop_log2=drop, good_round=0.0)
+    with psync.GpuRound(alg, n, seed=33 + n, schedule=sched, batch_capacity=count) as gr:
+        gr.load_inputs(90, count, init)
+        res = gr.run(90, count, per_instance=True)
+    osum, opi, orec = oracle_mod.run(gr.cfg, 90, count, init=init, per_instance=True, records=True)
+    _cmp_summary(res.summary, osum, gr.cfg.rounds)
+    assert [_inst_tuple(s) for s in res.per_instance] == [_inst_tuple(s) for s in opi]
+    # the mmor path ran: most instances end with some x different from its initial value
+    moved = sum(any(orec[i * n + p].final_x != init[i][p] for p in range(n)) for i in range(count))
+    assert moved > count // 2, moved
+
+
 @pytest.mark.parametrize("alg,n", [(psync.FloodMin(5), 256), (psync.FloodMin(3), 100), (psync.BenOr(), 128),
                                    (psync.KSetAgreement(2), 256), (psync.KSetAgreement(3), 90),
                                    (psync.KSetEarlyStopping(16, 2), 256)],
