@@ -127,7 +127,21 @@ PSG_DEV void otr_body(const KArgs& a) {
   PhaseTimers pt;  // profiling builds only: t0 setup, t1 active round, t2 frozen round, t3 finish
   pt.start();
   InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
-  for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
+  // Host-supplied initial values are loaded one instance ahead: the next row's load is
+  // issued when an instance starts and consumed when the next one does, so its latency
+  // overlaps the current instance's rounds instead of stalling its setup.
+  auto load_x0 = [&](uint64_t ii) -> int32_t {
+    if (ii == Q.kDone || !a.init || !g.valid) return 0;
+    const uint64_t in_ = a.ids ? a.ids[ii] : a.inst_begin + ii;
+    return a.init[init_row(a, ii, in_) * (uint64_t)n + g.pid];
+  };
+  uint64_t inext = Q.take(a);
+  int32_t x0next = load_x0(inext);
+  while (inext != Q.kDone) {
+    const uint64_t i = inext;
+    const int32_t x0host = x0next;
+    inext = Q.take(a);
+    x0next = load_x0(inext);
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;
     sc.setup(a, inst, g.pid, g.valid);
@@ -135,7 +149,7 @@ PSG_DEV void otr_body(const KArgs& a) {
     if (sc.crash_on) cs.prep(g, crl, sc.crash_round);
     sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
-    if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_OTR);
+    if (g.valid) x0 = a.init ? x0host : sc.init_value(g.pid, PSG_ALG_OTR);
     X0Set<W> X0;
     X0.build(g, x0tab[grp], x0);
     // OtrProcess state after init(io) (Otr.scala:15-26); flags are 0/1 lane words
