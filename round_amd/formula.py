@@ -1239,7 +1239,7 @@ def _fused_source(alg: int, waves: Sequence[int]) -> str:
     out = [f'#include "{src}"  // its kernel bodies; host launchers are compiled out (PSG_FUSED_MODULE)']
     # occupancy target of the W = 1 kernels (0: the compiler's); LastVoting's generated check
     # otherwise takes 92 VGPRs (5 waves/SIMD): 6 measured 155.6 -> 147.5 ms on C3 (7: no gain)
-    wpe = int(os.environ.get("PSG_FUSED_WPE", FUSED_WPE.get(alg, 0)))
+    wpe = int(os.environ.get("PSG_FUSED_WPE") or FUSED_WPE.get(alg, 0))
     for W in waves:
         threads = 256 if W == 1 else 64 * W
         attr = f"__attribute__((amdgpu_waves_per_eu({wpe}))) " if W == 1 and wpe > 0 else ""
