@@ -8,14 +8,21 @@ Agreement/Validity/Integrity/Irrevocability properties (+ Termination round)
 are evaluated. A step = one psg_run_batch over the GPU's instance shard with
 its initial values already resident in HBM.
 
-Multi-GPU: one process per GPU (torchrun); rank r owns global instance ids
-[r*I, (r+1)*I) (weak scaling); the per-batch int64 counters are all-reduced
-with RCCL (torch.distributed backend "nccl"). Timing: barrier +
+Multi-GPU: one process per GPU; rank r owns global instance ids [r*I, (r+1)*I)
+(weak scaling); the per-batch int64 counters are all-reduced with RCCL
+(torch.distributed backend "nccl"). `--gpus N` under torchrun uses the ranks it
+was given; `--gpus N` (N > 1) started directly launches N ranks itself, as a
+child `torch.distributed.run` started before anything touches the GPU.
+`--device-list 0,1,...` instead runs ONE process whose psg context spans the
+listed devices (psg_config.devices, one host thread per device — the JVM's route,
+psync/runtime/Runtime.scala:43-57), I instances per device. Timing: barrier +
 torch.cuda.synchronize() on both sides of exactly K steps, max over ranks.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,7 +41,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 CUS = 256  # MI355X compute units (8 XCDs x 32)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -47,7 +54,58 @@ def parse():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--device-list", default="",
+                    help="one process, one psg context over these HIP devices (e.g. 0,1,2,3)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="set up the ranks (gloo) and print the plan without touching a GPU")
+    return ap.parse_args(argv)
+
+
+def plan(args, env):
+    """How this invocation runs: ("ranks", world) under torchrun (WORLD_SIZE set),
+    ("launch", N) when --gpus N > 1 was asked without one (start N ranks as a child),
+    ("device-list", devices) for a single multi-device context, else ("single", 1)."""
+    if args.device_list:
+        devs = [int(x) for x in args.device_list.split(",") if x.strip()]
+        if not devs:
+            raise SystemExit("--device-list needs at least one device")
+        if "WORLD_SIZE" in env and int(env["WORLD_SIZE"]) > 1:
+            raise SystemExit("--device-list runs one process; do not combine it with torchrun ranks")
+        return "device-list", devs
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if args.gpus not in (1, world):
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the {world} ranks",
+                  file=sys.stderr)
+        return "ranks", world
+    if args.gpus > 1:
+        return "launch", args.gpus
+    return "single", 1
+
+
+def launch_cmd(argv, nproc, port):
+    """The child torchrun command line for `launch` mode (rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(argv, nproc, dry_run):
+    """Start `nproc` ranks as a child process and return its exit code. Runs before any
+    GPU call in this process (counting devices does not initialise the GPU here)."""
+    if not dry_run:
+        have = torch.cuda.device_count()
+        if have < nproc:
+            raise SystemExit(f"bench.py: --gpus {nproc} needs {nproc} visible GPUs, {have} found "
+                             "(--device-list runs several contexts in one process instead)")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(launch_cmd(argv, nproc, _free_port()), env=env)
 
 
 def lib_sha256():
@@ -102,47 +160,65 @@ def _time_oracle(oracle, cfg, threads, target_s):
     return s.process_rounds / dt, count, dt
 
 
+def host_cores():
+    """CPUs this process may really use: its affinity set, capped by the cgroup quota
+    (a 256-CPU affinity set under a 16-CPU quota is 16 cores)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = _cpu_quota()
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    return cores, aff, quota
+
+
 def cpu_baseline(cfg, target_s):
     """Time the oracle (C++ restatement of the reference's rounds + Spec, test
     infrastructure; not the JVM reference, which cannot run here) on the host: one
-    thread per core the process may run on (all of them, os.sched_getaffinity), and one
-    thread alone. SURVEY §8d / BASELINE.md §2 ask for both rates."""
+    thread per usable core (affinity capped by the cgroup quota), and one thread alone.
+    SURVEY §8d / BASELINE.md §2 ask for both rates."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.build()
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    quota = _cpu_quota()
+    cores, aff, quota = host_cores()
     v_all, n_all, t_all = _time_oracle(oracle, cfg, cores, target_s * 2 / 3)
     v_one, n_one, t_one = _time_oracle(oracle, cfg, 1, target_s / 3)
     return {
         "value": v_all,
         "unit": "process-rounds/s",
         "cores": cores,
+        "threads": cores,
         "kind": "port",
         "sample": f"{n_all} instances of the same workload (ids 0..{n_all - 1}), oracle/psg_oracle.cpp, "
                   f"{cores} threads, {t_all:.1f} s",
-        "single_core": {"value": v_one, "cores": 1,
+        "single_core": {"value": v_one, "cores": 1, "threads": 1,
                         "sample": f"{n_one} instances (ids 0..{n_one - 1}), 1 thread, {t_one:.1f} s"},
+        "affinity_cpus": aff,
         "cgroup_cpu_quota": quota,
         "note": "port = the build's C++ restatement of the reference (oracle/), not the JVM reference "
-                "(no JVM in the image; parity with the JVM is unpinned, DESIGN §7)",
+                "(no JVM in the image; parity with the JVM is unpinned, DESIGN §7); cores = "
+                "min(affinity CPUs, cgroup quota)",
     }
 
 
-def run_variant(rank, world, args, V, steps, warmup):
+def run_variant(rank, world, args, V, steps, warmup, devices=None):
+    """One timed series. Under ranks: this rank's shard on its LOCAL_RANK device. With a
+    device list: one context over `devices`, I instances per device."""
     dev = int(os.environ.get("LOCAL_RANK", 0))
-    I = args.instances
+    per = args.instances
     alg = psync.OTR()
     sched = psync.HOSchedule(drop_log2=3, good_round=0.25)
-    gr = psync.GpuRound(alg, args.n, rounds=args.rounds, seed=args.seed, schedule=sched, value_range=V,
-                        device=dev, batch_capacity=I)
-    begin, _ = rdist.shard(rank, world, I)
-    gr.load_inputs(begin, I)  # inputs resident in HBM before timing
+    if devices:
+        begin, count = 0, per * len(devices)
+        gr = psync.GpuRound(alg, args.n, rounds=args.rounds, seed=args.seed, schedule=sched, value_range=V,
+                            devices=devices, batch_capacity=count)
+    else:
+        (begin, count) = rdist.shard(rank, world, per)
+        gr = psync.GpuRound(alg, args.n, rounds=args.rounds, seed=args.seed, schedule=sched, value_range=V,
+                            device=dev, batch_capacity=count)
+    gr.load_inputs(begin, count)  # inputs resident in HBM before timing
     for _ in range(warmup):
-        gr.run(begin, I)
+        gr.run(begin, count)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -150,50 +226,80 @@ def run_variant(rank, world, args, V, steps, warmup):
     kns = 0
     last = None
     for _ in range(steps):
-        last = gr.run(begin, I)
+        last = gr.run(begin, count)
         kns += last.summary.kernel_ns
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     # node-level result: all-reduce (sum) the int64 counters over RCCL; max of the clocks
-    total = rdist.allreduce_summary(last.summary, device=f"cuda:{dev}")
-    dt_max = rdist.allreduce_max(dt, device=f"cuda:{dev}")
-    kernel_s = rdist.allreduce_max(kns / max(steps, 1) / 1e9, device=f"cuda:{dev}")
+    cuda = f"cuda:{dev}"
+    total = rdist.allreduce_summary(last.summary, device=cuda)
+    dt_max = rdist.allreduce_max(dt, device=cuda)
+    my_kernel_s = kns / max(steps, 1) / 1e9
+    per_rank = rdist.allgather_float(my_kernel_s, rank, world, device=cuda)
     cfg = gr.cfg
     gr.close()
-    return {"summary": total, "dt": dt_max, "kernel_s": kernel_s, "cfg": cfg}
+    return {"summary": total, "dt": dt_max, "kernel_s": max(per_rank), "per_rank_kernel_s": per_rank, "cfg": cfg}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def dry_run(mode, world, rank, args):
+    """--dry-run: the ranks exist and can all-reduce (gloo), nothing touches a GPU."""
+    if mode == "ranks":
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t.item())
+        dist.destroy_process_group()
+    else:
+        seen = 1
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "mode": mode, "world": world, "ranks_seen": seen,
+                          "n_gpus": world if mode != "device-list" else len(args.device_list.split(","))}),
+              flush=True)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    mode, what = plan(args, os.environ)
+    if mode == "launch":  # N ranks as a child torchrun, before any GPU call here
+        sys.exit(launch_ranks(argv, what, args.dry_run))
+    world = what if mode == "ranks" else 1
+    devices = what if mode == "device-list" else None
     rank = int(os.environ.get("RANK", "0"))
+    if args.dry_run:
+        return dry_run(mode, world, rank, args)
     dev = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(dev)
-    launched = "WORLD_SIZE" in os.environ  # torchrun: always go through RCCL, even at world size 1
+    launched = mode == "ranks"  # torchrun: always go through RCCL, even at world size 1
     if launched:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
-    head = run_variant(rank, world, args, args.V, args.steps, args.warmup)
+    n_gpus = len(devices) if devices else world
+    head = run_variant(rank, world, args, args.V, args.steps, args.warmup, devices)
     variants = {}
     for v in [int(x) for x in args.variants.split(",") if x]:
-        r = run_variant(rank, world, args, v, max(1, args.steps // 2), 1)
+        r = run_variant(rank, world, args, v, max(1, args.steps // 2), 1, devices)
         pr = r["summary"].process_rounds * max(1, args.steps // 2)
         variants[f"V={v}"] = {"value": pr / r["dt"], "kernel_ms": r["kernel_s"] * 1e3,
                               "violations": psync.BatchResult(psync.OTR(), args.rounds, r["summary"]).violations()}
     if rank == 0:
         s = head["summary"]
         steps = args.steps
-        pr_per_step = s.process_rounds  # all ranks, one step
+        pr_per_step = s.process_rounds  # all ranks / devices, one step
         value = pr_per_step * steps / head["dt"]
-        per_launch_pr = args.instances * args.n * args.rounds  # one rank's launch
+        per_launch_pr = args.instances * args.n * args.rounds  # one GPU's launch
         inst_rounds = args.instances * args.rounds
         alg_gbs = per_launch_pr * B_ALG_OTR / head["kernel_s"] / 1e9
+        if devices:
+            par = f"one context over devices {devices} (psg_config.devices), {args.instances} instances each"
+        else:
+            par = f"instance-sharded x{world} ranks (RCCL all-reduce of counters)"
         out = {
             "metric": "checked process-rounds/sec (node), OTR n=64 w/ invariants; % HBM peak",
             "value": value,
             "unit": "process-rounds/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": steps,
             "warmup": args.warmup,
             "ms_per_step": head["dt"] / steps * 1e3,
@@ -211,8 +317,9 @@ def main():
                 "rounds": args.rounds,
                 "instances_per_gpu": args.instances,
                 "value_range": args.V,
-                "parallelism": f"instance-sharded x{world} (RCCL all-reduce of counters)",
+                "parallelism": par,
             },
+            "per_gpu_kernel_ms": [x * 1e3 for x in head["per_rank_kernel_s"]] if not devices else None,
             "roofline": {
                 # the fused kernel keeps process state on chip (real HBM traffic ~2 % of the
                 # algorithmic bytes): its binding resource is instruction issue
@@ -248,7 +355,7 @@ def main():
             src, d, same = prof
             rl = out["roofline"]
             # live rate of this run: the profile's instructions per instance-round (a property of
-            # the code, taken on the same libpsg.so when profile_matches_build) x the launch's
+            # the code, valid only for the libpsg.so it was taken on) x the launch's
             # instance-rounds / this run's kernel time; peak: one instruction per CU per cycle
             # (SALU) / per SIMD per 2 cycles (VALU, wave64 on a 32-lane SIMD) at the profile's clock
             ipr = d["per_instance_round"]
@@ -257,20 +364,25 @@ def main():
             valu = ipr["SQ_INSTS_VALU"] * inst_rounds / head["kernel_s"] / 1e9
             pk_s, pk_v = CUS * clk, CUS * 4 * clk / 2
             pipe = "SALU" if salu / pk_s >= valu / pk_v else "VALU"
-            rl.update({"pipe": pipe, "achieved": salu if pipe == "SALU" else valu,
-                       "peak": pk_s if pipe == "SALU" else pk_v, "unit": f"G {pipe} instructions/s"})
-            rl["frac"] = rl["achieved"] / rl["peak"]
-            rl["valu"] = {"achieved": valu, "peak": pk_v, "frac": valu / pk_v, "unit": "G VALU instructions/s"}
-            rl["salu"] = {"achieved": salu, "peak": pk_s, "frac": salu / pk_s, "unit": "G SALU instructions/s"}
-            rl["insts_per_instance_round"] = ipr
-            rl["profile_issue_utilization"] = d.get("issue_utilization")
             rl["profile"] = src
             rl["profile_matches_build"] = same
-            rl["traffic"] = d["hbm"]["traffic_bytes"] / head["kernel_s"] / 1e9
-            rl["traffic_unit"] = "GB/s"
-            rl["traffic_bytes_per_launch"] = d["hbm"]["traffic_bytes"]
-            rl["traffic_source"] = src + " (PMC FETCH_SIZE*2 + WRITE_SIZE per launch)"
-        if not args.no_cpu_baseline and world == 1:  # the host baseline is an N = 1 figure
+            rl["profile_issue_utilization"] = d.get("issue_utilization")
+            if same:
+                rl.update({"pipe": pipe, "achieved": salu if pipe == "SALU" else valu,
+                           "peak": pk_s if pipe == "SALU" else pk_v, "unit": f"G {pipe} instructions/s"})
+                rl["frac"] = rl["achieved"] / rl["peak"]
+                rl["valu"] = {"achieved": valu, "peak": pk_v, "frac": valu / pk_v, "unit": "G VALU instructions/s"}
+                rl["salu"] = {"achieved": salu, "peak": pk_s, "frac": salu / pk_s, "unit": "G SALU instructions/s"}
+                rl["insts_per_instance_round"] = ipr
+                rl["traffic"] = d["hbm"]["traffic_bytes"] / head["kernel_s"] / 1e9
+                rl["traffic_unit"] = "GB/s"
+                rl["traffic_bytes_per_launch"] = d["hbm"]["traffic_bytes"]
+                rl["traffic_source"] = src + " (PMC FETCH_SIZE*2 + WRITE_SIZE per launch)"
+            else:
+                # counters of another build say nothing about this one's rates
+                rl["stale_profile"] = "profile taken on a different libpsg.so: achieved / frac / traffic " \
+                                      "left null; profile_issue_utilization is that build's own figure"
+        if not args.no_cpu_baseline and n_gpus == 1:  # the host baseline is an N = 1 figure
             out["cpu_baseline"] = cpu_baseline(head["cfg"], args.cpu_seconds)
         else:
             out["cpu_baseline"] = None

@@ -276,6 +276,11 @@ int psg_run_batch(psg_ctx* ctx, uint64_t inst_begin, uint64_t inst_count,
  * int32 and decision_round [count][n] int32 (-1 = none). Either may be NULL. */
 int psg_copy_decisions(psg_ctx* ctx, int32_t* decision, int32_t* decision_round);
 
+/* The instance count of the last batch (psg_run_batch / psg_run_batch_spec, 0 after an
+ * empty one): the [count][n] size psg_copy_decisions writes. The library's own record, so
+ * a binding sizing host arrays (the JNI shim) never trusts a copy of its own. */
+int psg_last_batch_count(const psg_ctx* ctx, uint64_t* count);
+
 /* Re-execute the listed global instance ids and return their summaries (k
  * entries) and per-process records (k * n entries, nullable). Inputs: the staged
  * ones (psg_load_inputs) when every id lies in the staged range, else seeded;
@@ -301,7 +306,9 @@ int psg_run_batch_spec(psg_ctx* ctx, uint64_t inst_begin, uint64_t inst_count, c
  * alg (enum psg_alg, 0 = unchecked) restricts the fields to the algorithm's state and is
  * recorded in out->alg. The arrays are the library's: release them with psg_spec_release.
  * names (nullable) receives the slot names, '\n'-separated ("Safety", "Invariant0", ...,
- * the property names, "SafetyPredicate"); err (nullable) the reason of a failure. */
+ * the property names, "SafetyPredicate"); PSG_ERANGE (nothing allocated) when names_len is
+ * too small for all of them, err then says how many bytes are needed. Text nested deeper
+ * than 512 forms is refused (PSG_EINVAL). err (nullable) the reason of a failure. */
 int psg_spec_from_text(const char* text, int32_t alg, psg_spec_program* out, char* names, size_t names_len,
                        char* err, size_t err_len);
 void psg_spec_release(psg_spec_program* prog);

@@ -31,7 +31,6 @@
 typedef struct jctx {
   psg_ctx* ctx;
   int64_t n, rounds, words; /* words = ceil(n / 64) */
-  int64_t last_count;       /* instances of the last batch (copyDecisions) */
 } jctx;
 
 static void throw_cls(JNIEnv* env, const char* cls, const char* msg) {
@@ -63,6 +62,14 @@ static int check_len(JNIEnv* env, jarray arr, int64_t need, int nullable, const 
     return 0;
   }
   return 1;
+}
+
+/* Cells of the last batch's [count][n] decision arrays, from the library's own record
+ * (psg_last_batch_count): an empty batch after a large one yields 0, never a stale size. */
+static int64_t last_cells(const jctx* j) {
+  uint64_t count = 0;
+  if (psg_last_batch_count(j->ctx, &count)) return 0;
+  return (int64_t)count * j->n;
 }
 
 static jctx* J(JNIEnv* env, jlong h) {
@@ -181,7 +188,6 @@ JNIEXPORT jlongArray JNICALL Java_psync_gpu_GpuRoundNative_00024_runBatch(JNIEnv
     throw_psg(env, rc, psg_last_error(j->ctx));
     return NULL;
   }
-  j->last_count = count;
   if (pi) {
     (*env)->SetByteArrayRegion(env, perInst, 0, (jsize)(sizeof(psg_instance_summary) * (size_t)count),
                                (const jbyte*)pi);
@@ -237,7 +243,6 @@ JNIEXPORT jlongArray JNICALL Java_psync_gpu_GpuRoundNative_00024_runBatchSpec(
     throw_psg(env, rc, rc == PSG_ENOMEM ? "out of host memory" : psg_last_error(j->ctx));
     return NULL;
   }
-  j->last_count = count;
   if (pi) {
     (*env)->SetByteArrayRegion(env, perInst, 0, (jsize)(sizeof(psg_instance_summary) * (size_t)count),
                                (const jbyte*)pi);
@@ -289,15 +294,33 @@ JNIEXPORT jstring JNICALL Java_psync_gpu_GpuRoundNative_00024_compileSpecNames(J
   }
   const char* t = (*env)->GetStringUTFChars(env, text, NULL);
   psg_spec_program p;
-  char names[4096], err[512];
-  const int rc = psg_spec_from_text(t, alg, &p, names, sizeof names, err, sizeof err);
+  char err[512];
+  /* PSG_ERANGE = the buffer cannot hold every slot name: grow it, never truncate (the
+   * names must line up with compileSpec's slotEntry / slotFlags) */
+  size_t len = 4096;
+  char* names = NULL;
+  int rc = PSG_ERANGE;
+  while (rc == PSG_ERANGE && len <= ((size_t)1 << 24)) {
+    char* grown = (char*)realloc(names, len);
+    if (!grown) {
+      rc = PSG_ENOMEM;
+      snprintf(err, sizeof err, "out of host memory");
+      break;
+    }
+    names = grown;
+    rc = psg_spec_from_text(t, alg, &p, names, len, err, sizeof err);
+    len *= 2;
+  }
   (*env)->ReleaseStringUTFChars(env, text, t);
   if (rc) {
+    free(names);
     throw_psg(env, rc, err);
     return NULL;
   }
   psg_spec_release(&p);
-  return (*env)->NewStringUTF(env, names);
+  jstring out = (*env)->NewStringUTF(env, names);
+  free(names);
+  return out;
 }
 
 /* void copyDecisions(long ctx, int[] decision, int[] decisionRound) — the batched
@@ -306,7 +329,7 @@ JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_copyDecisions(JNIEnv*
                                                                          jintArray dec, jintArray drnd) {
   (void)self;
   jctx* j = J(env, h);
-  const int64_t cells = j ? j->last_count * j->n : 0;
+  const int64_t cells = j ? last_cells(j) : 0;
   if (!j || !check_len(env, dec, cells, 1, "decision") || !check_len(env, drnd, cells, 1, "decisionRound")) return;
   jint* d = dec ? (*env)->GetIntArrayElements(env, dec, NULL) : NULL;
   jint* r = drnd ? (*env)->GetIntArrayElements(env, drnd, NULL) : NULL;
@@ -355,7 +378,7 @@ JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_copyDecisionsF64(JNIE
                                                                             jdoubleArray dec, jintArray round) {
   (void)self;
   jctx* j = J(env, h);
-  const int64_t cells = j ? j->last_count * j->n : 0;
+  const int64_t cells = j ? last_cells(j) : 0;
   if (!j || !check_len(env, dec, cells, 1, "decision") || !check_len(env, round, cells, 1, "decisionRound")) return;
   jdouble* d = dec ? (*env)->GetDoubleArrayElements(env, dec, NULL) : NULL;
   jint* r = round ? (*env)->GetIntArrayElements(env, round, NULL) : NULL;

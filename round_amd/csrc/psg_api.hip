@@ -627,8 +627,12 @@ int psg_load_inputs_f64(psg_ctx* c, uint64_t inst_begin, uint64_t count, const d
 static int multi_run(psg_ctx* c, uint64_t inst_begin, uint64_t count, const psg_spec_program* prog, psg_summary* out,
                      psg_instance_summary* per_inst) {
   if (out) std::memset(out, 0, sizeof(*out));
-  if (count == 0) return PSG_OK;
   if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
+  if (count == 0) {  // the library's "last batch" is the single source of truth (JNI checks use it)
+    c->last_count = 0;
+    for (psg_ctx* s : c->subs) s->last_count = 0;
+    return PSG_OK;
+  }
   if (c->ho_loaded && (inst_begin != c->ho_begin || count != c->ho_count))
     return fail(c, PSG_ERANGE, "a multi-device run under an explicit schedule covers exactly the loaded range");
   if (!(c->staged && c->staged_begin == inst_begin && c->staged_count == count)) {
@@ -654,11 +658,12 @@ static int multi_run(psg_ctx* c, uint64_t inst_begin, uint64_t count, const psg_
 int psg_run_batch(psg_ctx* c, uint64_t inst_begin, uint64_t count, psg_summary* out, psg_instance_summary* per_inst) {
   if (!c) return PSG_EINVAL;
   if (!c->subs.empty()) return multi_run(c, inst_begin, count, nullptr, out, per_inst);
+  if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
   if (count == 0) {
     if (out) std::memset(out, 0, sizeof(*out));
+    c->last_count = 0;
     return PSG_OK;
   }
-  if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
   if (int rc = check_sched_range(c, inst_begin, count)) return rc;
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (!(c->staged && c->staged_begin == inst_begin && c->staged_count == count)) {
@@ -747,6 +752,12 @@ static uint32_t prog_fields(const psg_spec_program* p) {
   return m & ((1u << PSG_NFIELDS) - 1u);
 }
 
+int psg_last_batch_count(const psg_ctx* c, uint64_t* count) {
+  if (!c || !count) return PSG_EINVAL;
+  *count = c->last_count;
+  return PSG_OK;
+}
+
 int psg_copy_decisions(psg_ctx* c, int32_t* decision, int32_t* decision_round) {
   if (!c) return PSG_EINVAL;
   if (!c->subs.empty()) {  // the last batch's slices, in device order
@@ -754,6 +765,7 @@ int psg_copy_decisions(psg_ctx* c, int32_t* decision, int32_t* decision_round) {
     for (size_t d = 0; d < nd; ++d) {
       uint64_t off, m;
       split(c->last_count, nd, d, off, m);
+      if (!m) continue;  // an empty slice: the device ran nothing (its own last_count is 0)
       const int rc = psg_copy_decisions(c->subs[d], decision ? decision + off * n : nullptr,
                                         decision_round ? decision_round + off * n : nullptr);
       if (rc) return fail(c, rc, "device " + std::to_string(c->cfg.devices[d]) + ": " + c->subs[d]->err);
@@ -787,7 +799,10 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
   if (count > c->cap) return fail(c, PSG_ERANGE, "inst_count exceeds batch_capacity");
   if (int rc = check_sched_range(c, inst_begin, count)) return rc;
   if (out) std::memset(out, 0, sizeof(*out));
-  if (count == 0) return PSG_OK;
+  if (count == 0) {
+    c->last_count = 0;
+    return PSG_OK;
+  }
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const int n = c->cfg.n, R = c->cfg.rounds;
   // program: code | slot_entry | slot_flags
@@ -982,6 +997,7 @@ int psg_copy_decisions_f64(psg_ctx* c, double* decision, int32_t* decision_round
     for (size_t d = 0; d < nd; ++d) {
       uint64_t off, m;
       split(c->last_count, nd, d, off, m);
+      if (!m) continue;
       const int rc = psg_copy_decisions_f64(c->subs[d], decision ? decision + off * n : nullptr,
                                             decision_round ? decision_round + off * n : nullptr);
       if (rc) return fail(c, rc, "device " + std::to_string(c->cfg.devices[d]) + ": " + c->subs[d]->err);

@@ -48,6 +48,8 @@ struct Sx {
 
 struct Reader {
   const char* p;
+  int depth = 0;  // nesting of the form being read: deep text must not overflow the native stack
+  static constexpr int kMaxDepth = 512;
   void skip() {
     while (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r') ++p;
   }
@@ -56,12 +58,14 @@ struct Reader {
     Sx s;
     if (!*p) throw SpecError("Formula text: unexpected end");
     if (*p == '(') {
+      if (++depth > kMaxDepth) throw SpecError("Formula text: nesting deeper than 512 forms");
       ++p;
       for (;;) {
         skip();
         if (!*p) throw SpecError("Formula text: missing )");
         if (*p == ')') {
           ++p;
+          --depth;
           return s;
         }
         s.items.push_back(read());
@@ -650,6 +654,11 @@ int psg_spec_from_text(const char* text, int32_t alg, psg_spec_program* out, cha
     out->alg = alg;
     std::string joined;
     for (size_t k = 0; k < c.names.size(); ++k) joined += (k ? "\n" : "") + c.names[k];
+    if (names && names_len <= joined.size()) {  // never a silently truncated slot-name list
+      psg_spec_release(out);
+      put(err, err_len, "names buffer too small: " + std::to_string(joined.size() + 1) + " bytes needed");
+      return PSG_ERANGE;
+    }
     put(names, names_len, joined);
     put(err, err_len, "");
     return PSG_OK;

@@ -45,3 +45,13 @@ def allreduce_max(x: float, device=None) -> float:
     if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def allgather_float(x: float, rank: int, world: int, device=None) -> list:
+    """Every rank's value of x, in rank order (a zero vector with this rank's slot set,
+    summed over ranks)."""
+    t = torch.zeros(world, dtype=torch.float64, device=device if device is not None else "cpu")
+    t[rank] = x
+    if dist.is_available() and dist.is_initialized() and world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.cpu().tolist()]

@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("PSG_LIB") or os.path.join(HERE, "libpsg.so")  # PSG_L
 
 EXPORTED_SYMBOLS = [
     "psg_config_default", "psg_check_count", "psg_check_name", "psg_alg_from_class",
-    "psg_create", "psg_load_inputs", "psg_run_batch", "psg_copy_decisions",
+    "psg_create", "psg_load_inputs", "psg_run_batch", "psg_copy_decisions", "psg_last_batch_count",
     "psg_fetch_instances", "psg_last_error", "psg_destroy", "psg_create_error",
     "psg_selftest_map_head", "psg_load_inputs_f64", "psg_copy_decisions_f64", "psg_fetch_instances_f64",
     "psg_run_batch_spec", "psg_load_schedule", "psg_clear_schedule", "psg_materialize_schedule",
@@ -55,6 +55,7 @@ def load():
     L.psg_run_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(abi.Summary),
                                 C.POINTER(abi.InstanceSummary)]
     L.psg_copy_decisions.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    L.psg_last_batch_count.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     L.psg_fetch_instances.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t,
                                       C.POINTER(abi.InstanceSummary), C.POINTER(abi.ProcessRecord)]
     L.psg_last_error.argtypes = [C.c_void_p]
@@ -96,7 +97,6 @@ class Context:
         if rc != 0:
             raise PsgError(rc, L.psg_create_error().decode())
         self._h = h
-        self._last_count = 0
 
     def _check(self, rc):
         if rc != 0:
@@ -134,7 +134,6 @@ class Context:
         s = abi.Summary()
         pi = (abi.InstanceSummary * count)() if per_instance else None
         self._check(load().psg_run_batch(self._h, inst_begin, count, C.byref(s), pi))
-        self._last_count = count
         return s, (list(pi) if pi is not None else None)
 
     def run_batch_np(self, inst_begin, count):
@@ -146,13 +145,18 @@ class Context:
         pi = np.zeros(count, SUMMARY_DTYPE)
         ptr = pi.ctypes.data_as(C.POINTER(abi.InstanceSummary))
         self._check(load().psg_run_batch(self._h, inst_begin, count, C.byref(s), ptr))
-        self._last_count = count
         return s, pi
+
+    def last_batch_count(self) -> int:
+        """Instances of the last batch, the library's own record (psg_last_batch_count)."""
+        k = C.c_uint64()
+        self._check(load().psg_last_batch_count(self._h, C.byref(k)))
+        return int(k.value)
 
     def copy_decisions_np(self):
         """(decision, decision_round) of the last batch as numpy [count][n] arrays."""
         import numpy as np
-        shape = (self._last_count, self.cfg.n)
+        shape = (self.last_batch_count(), self.cfg.n)
         dr = np.zeros(shape, np.int32)
         pdr = dr.ctypes.data_as(C.POINTER(C.c_int32))
         if self.real:
@@ -182,13 +186,12 @@ class Context:
         pi = (abi.InstanceSummary * count)() if per_instance else None
         cp = program.to_c()
         self._check(load().psg_run_batch_spec(self._h, inst_begin, count, C.byref(cp), C.byref(s), pi))
-        self._last_count = count
         return s, (list(pi) if pi is not None else None)
 
     def copy_decisions(self):
         """(decision, decision_round) of the last batch, [count*n] each (Double decisions
         for real-valued algorithms)."""
-        cells = self._last_count * self.cfg.n
+        cells = self.last_batch_count() * self.cfg.n
         dr = (C.c_int32 * cells)()
         if self.real:
             dec = (C.c_double * cells)()
@@ -321,9 +324,14 @@ def spec_from_text(text, alg=0):
     from . import formula
     L = load()
     cp = abi.SpecProgram()
-    names = C.create_string_buffer(4096)
     err = C.create_string_buffer(1024)
-    rc = L.psg_spec_from_text(text.encode(), int(alg), C.byref(cp), names, len(names), err, len(err))
+    size = 4096
+    while True:  # PSG_ERANGE: the slot names need a larger buffer (never truncated)
+        names = C.create_string_buffer(size)
+        rc = L.psg_spec_from_text(text.encode(), int(alg), C.byref(cp), names, len(names), err, len(err))
+        if rc != abi.PSG_ERANGE or size >= 1 << 24:
+            break
+        size *= 4
     if rc != 0:
         raise formula.FormulaError(err.value.decode() or f"psg_spec_from_text rc={rc}")
     try:

@@ -157,12 +157,11 @@ int fj_take_oob(void) {
   return r;
 }
 /* a context handle of the shim's layout with no psg context behind it (argument-check tests) */
-typedef struct { void* ctx; long long n, rounds, words, last_count; } fj_jctx;
-void* fj_fake_ctx(int n, int rounds, long long last_count) {
+typedef struct { void* ctx; long long n, rounds, words; } fj_jctx;
+void* fj_fake_ctx(int n, int rounds) {
   fj_jctx* j = (fj_jctx*)calloc(1, sizeof(fj_jctx));
   j->n = n;
   j->rounds = rounds;
   j->words = (n + 63) / 64;
-  j->last_count = last_count;
   return j;
 }

@@ -1,0 +1,64 @@
+"""bench.py's launch logic (CPU): `--gpus N` must really run N ranks.
+
+`plan()` decides how an invocation runs; `--dry-run` sets the ranks up over gloo and
+prints the plan without touching a GPU, so the child-torchrun path is exercised end to
+end here."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def _args(*a):
+    return bench.parse(list(a))
+
+
+def test_plan_modes():
+    assert bench.plan(_args(), {}) == ("single", 1)
+    assert bench.plan(_args("--gpus", "1"), {}) == ("single", 1)
+    assert bench.plan(_args("--gpus", "8"), {}) == ("launch", 8)
+    assert bench.plan(_args("--gpus", "8"), {"WORLD_SIZE": "8"}) == ("ranks", 8)
+    assert bench.plan(_args("--gpus", "1"), {"WORLD_SIZE": "1"}) == ("ranks", 1)
+    assert bench.plan(_args("--device-list", "0,1,2,3"), {}) == ("device-list", [0, 1, 2, 3])
+    with pytest.raises(SystemExit):
+        bench.plan(_args("--device-list", "0,1"), {"WORLD_SIZE": "2"})
+
+
+def test_launch_command_shape():
+    cmd = bench.launch_cmd(["--gpus", "4", "--steps", "3"], 4, 29555)
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd and "--master-port=29555" in cmd
+    assert cmd[-5].endswith("bench.py") and cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+
+
+def test_gpus_two_spawns_two_ranks():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d == {"dry_run": True, "mode": "ranks", "world": 2, "ranks_seen": 2, "n_gpus": 2}
+
+
+def test_gpus_beyond_visible_devices_fails_loudly(monkeypatch):
+    """Never a silent n_gpus = 1 when more were asked for."""
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 1)
+    with pytest.raises(SystemExit, match="needs 4 visible GPUs"):
+        bench.launch_ranks(["--gpus", "4"], 4, dry_run=False)
+
+
+def test_host_cores_respects_quota(monkeypatch):
+    monkeypatch.setattr(bench, "_cpu_quota", lambda: 16.0)
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(256)))
+    assert bench.host_cores() == (16, 256, 16.0)
+    monkeypatch.setattr(bench, "_cpu_quota", lambda: None)
+    assert bench.host_cores()[0] == 256

@@ -90,3 +90,28 @@ def test_bench_under_torchrun_world1():
     assert d["n_gpus"] == 1 and d["value"] > 0
     assert d["checks"]["process_rounds_counted"] == 200000 * 64 * 20
     assert all(v == 0 for v in d["checks"]["violations"].values())
+
+
+def test_bench_device_list_two_devices():
+    """`bench.py --device-list 0,0` runs one context over two device slots
+    (psg_config.devices), reports n_gpus = 2, and its node counters equal one context over
+    the same 2 x I instances."""
+    per = 100_000
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device-list", "0,0", "--steps", "2", "--warmup", "1",
+           "--instances", str(per), "--variants=", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    c = d["checks"]
+    assert c["process_rounds_counted"] == 2 * per * 64 * 20
+    with psync.GpuRound(psync.OTR(), 64, rounds=20, seed=2, value_range=64,
+                        schedule=psync.HOSchedule(drop_log2=3, good_round=0.25), device=0,
+                        batch_capacity=2 * per) as gr:
+        s = gr.run(0, 2 * per).summary
+    assert c["decided_processes"] == s.decided_processes
+    assert c["termination_hist"] == [s.term_hist[i] for i in range(22)]
+    assert c["process_rounds_active"] == s.active_process_rounds
+    assert c["instance_rounds_live"] == s.live_instance_rounds

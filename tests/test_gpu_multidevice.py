@@ -133,3 +133,27 @@ def test_spec_program_algorithm_mismatch():
     with psync.GpuRound(psync.OTR(), 64, seed=1, batch_capacity=64) as g:
         fused.alg = abi.PSG_ALG_OTR
         g.run_spec(0, 64, fused)
+
+
+@pytest.mark.parametrize("alg,n,kw", [(psync.OTR(), 64, dict(value_range=64, seed=2)),
+                                      (psync.EpsilonConsensus(5, 1e-6), 64, dict(seed=62))],
+                         ids=["otr", "epsilon-f64"])
+def test_multi_small_batch_after_large(alg, n, kw):
+    """a batch smaller than the device list leaves some device an empty
+    slice; its decisions from an earlier, larger batch must not be copied (the host buffer
+    is sized from the new count). Large batch, then 1 instance, then 0, on [0, 0]."""
+    big, begin = 1000, 77
+    with psync.GpuRound(alg, n, batch_capacity=big, **kw) as one:
+        one.run(begin, 1)
+        d_one = one.decisions()
+    with psync.GpuRound(alg, n, batch_capacity=big, devices=[0, 0], **kw) as many:
+        many.run(begin, big)
+        assert many._ctx.last_batch_count() == big
+        many.run(begin, 1)
+        assert many._ctx.last_batch_count() == 1
+        dec, dr = many.decisions()
+        assert len(dec) == n and len(dr) == n
+        assert [float(x).hex() for x in dec] == [float(x).hex() for x in d_one[0]] and dr == d_one[1]
+        many.run(begin, 0)
+        assert many._ctx.last_batch_count() == 0
+        assert many.decisions() == ([], [])

@@ -84,7 +84,7 @@ class Shim:
         L.fj_len.argtypes = [C.c_void_p]
         L.fj_free.argtypes = [C.c_void_p]
         L.fj_fake_ctx.restype = C.c_void_p
-        L.fj_fake_ctx.argtypes = [C.c_int, C.c_int, C.c_longlong]
+        L.fj_fake_ctx.argtypes = [C.c_int, C.c_int]
         self.env = L.fj_env()
 
     def fn(self, name, restype, *argtypes):
@@ -120,7 +120,7 @@ def shim():
 
 def test_short_arrays_are_refused(shim):
     """ADVICE: the shim checks every Java array's length before taking its elements."""
-    h = shim.L.fj_fake_ctx(64, 20, 10)  # n = 64, R = 20, last batch 10 instances; no psg context behind it
+    h = shim.L.fj_fake_ctx(64, 20)  # n = 64, R = 20; no psg context behind it
     load = shim.fn("loadInputs", None, C.c_int64, C.c_int64, C.c_int64, C.c_void_p)
     load(h, 0, 10, shim.array(FJ_INT, [1] * (10 * 64 - 1)))
     exc = shim.exception()
@@ -133,9 +133,11 @@ def test_short_arrays_are_refused(shim):
     assert "2559 elements, 2560 needed" in shim.exception()[1]
     sched(h, 0, 2, shim.array(FJ_LONG, [0] * (2 * 20 * 64)), shim.array(FJ_INT, [0] * 127))
     assert "crash has 127 elements, 128 needed" in shim.exception()[1]
+    # copyDecisions sizes its check from the library's own last batch (psg_last_batch_count):
+    # with no context behind the handle that is 0 cells, and the C ABI refuses the null context
     copy = shim.fn("copyDecisions", None, C.c_int64, C.c_void_p, C.c_void_p)
-    copy(h, shim.array(FJ_INT, [0] * 639), None)
-    assert "decision has 639 elements, 640 needed" in shim.exception()[1]
+    copy(h, shim.array(FJ_INT, []), None)
+    assert shim.exception()[1].startswith("psg error -22")
     fetch = shim.fn("fetch", None, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p)
     fetch(h, shim.array(FJ_LONG, [1, 2]), shim.array(FJ_BYTE, [0] * 48), shim.array(FJ_INT, [0] * (2 * 64 * 4 - 1)))
     assert "records has 511 elements, 512 needed" in shim.exception()[1]
@@ -214,6 +216,19 @@ def test_batch_through_the_shim_equals_the_python_binding(shim):
                                         shim.array(FJ_INT, packed[4 + nw:4 + nw + ns]),
                                         shim.array(FJ_INT, packed[4 + nw + ns:]), packed[2], packed[3],
                                         abi.PSG_ALG_OTR, None, None))
+        # after an empty batch the last batch holds 0 instances (an empty Java array
+        # is enough and nothing is written past it); a batch of 1 on a two-device list leaves
+        # one device with an empty slice, whose stale size must not be copied
+        run(h, begin, 0, None)
+        copy = shim.fn("copyDecisions", None, C.c_int64, C.c_void_p, C.c_void_p)
+        copy(h, shim.L.fj_new(FJ_INT, 0), shim.L.fj_new(FJ_INT, 0))
+        assert shim.exception() is None and shim.L.fj_take_oob() == 0
+        one, one_r = shim.L.fj_new(FJ_INT, n), shim.L.fj_new(FJ_INT, n)
+        run(h, begin, 1, None)
+        copy(h, one, one_r)
+        assert shim.exception() is None and shim.L.fj_take_oob() == 0
+        assert shim.values(FJ_INT, one) == shim.values(FJ_INT, dec)[:n]
+        assert shim.values(FJ_INT, one_r) == shim.values(FJ_INT, drd)[:n]
         shim.fn("destroy", None, C.c_int64)(h)
         assert shim.exception() is None and shim.L.fj_take_oob() == 0
         with psync.GpuRound(psync.OTR(), n, rounds=R, seed=2, value_range=V, batch_capacity=count) as g:

@@ -143,3 +143,27 @@ def test_text_programs_reproduce_the_oracle_checker(alg, nn, kw, oracle_mod):
     k = len(prog.slot_names)
     for i in range(cnt):
         assert ff[i] == list(pi[i].first_fail)[:k] and tm[i] == pi[i].term_round, i
+
+
+def test_names_buffer_too_small_is_an_error():
+    """slot names are never silently truncated (they must line up with slot_entry)."""
+    import ctypes as C
+    L = lib.load()
+    text = F.to_text(F.otr_spec())
+    cp, err = abi.SpecProgram(), C.create_string_buffer(512)
+    small = C.create_string_buffer(8)
+    rc = L.psg_spec_from_text(text.encode(), abi.PSG_ALG_OTR, C.byref(cp), small, len(small), err, len(err))
+    assert rc == abi.PSG_ERANGE and "bytes needed" in err.value.decode()
+    assert cp.n_words == 0 and not cp.code  # nothing allocated on the error path
+    need = int(err.value.decode().split(":")[1].split()[0])
+    exact = C.create_string_buffer(need)
+    assert L.psg_spec_from_text(text.encode(), abi.PSG_ALG_OTR, C.byref(cp), exact, need, err, len(err)) == 0
+    assert exact.value.decode().split("\n")[0] == "Safety"
+    L.psg_spec_release(C.byref(cp))
+
+
+def test_deep_nesting_is_refused_not_a_crash():
+    """text nested past 512 forms gets PSG_EINVAL instead of overflowing the stack."""
+    deep = "(Spec (invariants " + "(Not " * 100000 + "true" + ")" * 100000 + "))"
+    with pytest.raises(F.FormulaError, match="nesting deeper than 512"):
+        lib.spec_from_text(deep, abi.PSG_ALG_OTR)
