@@ -55,6 +55,9 @@ def lib():
         L.oracle_trace.argtypes = [C.POINTER(abi.Config), C.c_uint64, C.c_uint64, C.POINTER(C.c_int32),
                                    C.POINTER(C.c_int32), C.c_int32]
         L.oracle_trace.restype = C.c_int
+        L.oracle_trace_checks.argtypes = [C.POINTER(abi.Config), C.c_uint64, C.c_uint64, C.POINTER(C.c_int32),
+                                          C.POINTER(C.c_int32), C.POINTER(C.c_uint16), C.c_int32, C.c_int32]
+        L.oracle_trace_checks.restype = C.c_int
         L.oracle_vm_run.argtypes = [C.POINTER(abi.SpecProgram), C.POINTER(C.c_int32), C.c_uint64, C.c_int32,
                                     C.c_int32, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]
         L.oracle_vm_run.restype = C.c_int
@@ -233,6 +236,25 @@ def trace(cfg, inst_begin, count, init=None, threads=8):
         init_arr = (C.c_int32 * len(flat))(*flat)
     _check(lib().oracle_trace(C.byref(cfg), inst_begin, count, init_arr, out, threads))
     return out
+
+
+def trace_checks(cfg, inst_begin, count, init=None, threads=8, spec_mode=2):
+    """(trace, bits): the states of trace() as numpy int32 [count][R+1][9][n] and the
+    checker's verdict per check point, uint16 [count][R+1] (bit s = slot s holds, bit 15 =
+    Termination holds). spec_mode 0 hand-lowered, 1 Formula interpreter, 2 both (required
+    equal)."""
+    import numpy as np
+    R, n = cfg.rounds, cfg.n
+    tr = np.zeros((count, R + 1, NFIELDS, n), np.int32)
+    bits = np.zeros((count, R + 1), np.uint16)
+    init_arr = None
+    if init is not None:
+        init_arr = np.ascontiguousarray(init, np.int32)
+    _check(lib().oracle_trace_checks(C.byref(cfg), inst_begin, count,
+                                     init_arr.ctypes.data_as(C.POINTER(C.c_int32)) if init_arr is not None else None,
+                                     tr.ctypes.data_as(C.POINTER(C.c_int32)),
+                                     bits.ctypes.data_as(C.POINTER(C.c_uint16)), threads, spec_mode))
+    return tr, bits
 
 
 def vm_run(program, tr, count, n, rounds):

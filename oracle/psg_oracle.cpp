@@ -1286,6 +1286,7 @@ struct InstOut {
   std::vector<psg_process_record> rec;
   std::vector<double> fdec, fx; /* real-valued algorithms: Double decision / final x per process */
   std::vector<int32_t>* vtrace = nullptr; /* Spec-program trace: [R+1][F][n] int32, None = INT32_MIN */
+  std::vector<uint16_t>* ckbits = nullptr; /* per check point: bit s = slot s holds, bit 15 = Termination */
   std::vector<int64_t> trace; /* optional: per check point, per process F_X / decided */
   bool mismatch = false;
   std::string msg;
@@ -1386,6 +1387,11 @@ static void run_engine(Alg& alg, const psg_config& cfg, uint64_t inst, const int
     for (int i = 0; i < nck; ++i)
       if (!ck[i] && S.first_fail[i] == PSG_NEVER) S.first_fail[i] = (uint8_t)c;
     if (term && S.term_round == PSG_NEVER) S.term_round = (uint8_t)c;
+    if (out.ckbits) {
+      uint16_t b = term ? (uint16_t)0x8000 : (uint16_t)0;
+      for (int i = 0; i < nck; ++i) if (ck[i]) b |= (uint16_t)(1u << i);
+      out.ckbits->push_back(b);
+    }
     if (out.vtrace)
       for (int f = 0; f < F_NFIELDS; ++f)
         for (int p = 0; p < n; ++p)
@@ -1770,6 +1776,42 @@ int oracle_trace(const psg_config* cfg, uint64_t inst_begin, uint64_t count, con
   for (int t = 1; t < threads; ++t) th.emplace_back(worker, t);
   worker(0);
   for (auto& x : th) x.join();
+  return 0;
+}
+
+/* oracle_trace plus the checker's verdict at every check point: bits [count][R+1]
+ * (bit s = slot s holds at that check point, bit 15 = Termination holds), from the
+ * hand-lowered evaluator (spec_mode 0), the Formula interpreter (1) or both, required
+ * equal (2). trace (nullable) as oracle_trace. Test infrastructure: the per-check-point
+ * view the reference-model pins (tests/test_reference_otr_spec.py) compare against. */
+int oracle_trace_checks(const psg_config* cfg, uint64_t inst_begin, uint64_t count, const int32_t* init,
+                        int32_t* trace, uint16_t* bits, int32_t threads, int32_t spec_mode) {
+  std::string err;
+  int rc = orc::validate(cfg, err);
+  if (rc) { g_oracle_err = err; return rc; }
+  if (threads < 1) threads = 1;
+  const uint64_t per = (uint64_t)(cfg->rounds + 1) * orc::F_NFIELDS * (uint64_t)cfg->n;
+  std::vector<std::string> errs(threads);
+  auto worker = [&](int t) {
+    uint64_t lo = count * (uint64_t)t / threads, hi = count * (uint64_t)(t + 1) / threads;
+    for (uint64_t i = lo; i < hi; ++i) {
+      orc::InstOut o;
+      std::vector<int32_t> tr;
+      std::vector<uint16_t> ck;
+      o.vtrace = &tr;
+      o.ckbits = &ck;
+      orc::run_one(*cfg, inst_begin + i, init ? init + i * (uint64_t)cfg->n : nullptr, spec_mode, nullptr, o, false);
+      if (o.mismatch && errs[t].empty()) errs[t] = o.msg;
+      if (trace) std::memcpy(trace + i * per, tr.data(), sizeof(int32_t) * per);
+      std::memcpy(bits + i * (uint64_t)(cfg->rounds + 1), ck.data(), sizeof(uint16_t) * ck.size());
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t) th.emplace_back(worker, t);
+  worker(0);
+  for (auto& x : th) x.join();
+  for (auto& e : errs)
+    if (!e.empty()) { g_oracle_err = e; return PSG_EIO; }
   return 0;
 }
 
