@@ -2,7 +2,8 @@
 """Throughput of the other BASELINE.json configuration rows (the headline is bench.py).
 
   C3  LastVoting n=64, 1e8 instances over 8 GPUs (1.25e7 per GPU), 20 rounds, crash-stop
-  C4  FloodMin n=256 crash-stop sweep f in {0,1,2,4,...,64}, R = f+2; KSetAgreement n=256, k=2, R=16
+  C4  FloodMin n=256 crash-stop sweep f in {0,1,2,4,...,64}, R = f+2; KSetAgreement n=256, k=2, R=16,
+      the same sweep over f
   C5  BenOr n=128, 64 rounds, |HO(p)| > n/2; termination-round histogram all-reduced
   W2  second-wave algorithms: OTR2, ShortLastVoting, KSetEarlyStopping, EpsilonConsensus
 
@@ -19,6 +20,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402  (first: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
@@ -35,7 +37,9 @@ def configs(scale):
     out = [("C3_lastvoting_n64", psync.LastVoting(), 64, int(12_500_000 * s), {}, 42)]
     for f in (0, 1, 2, 4, 8, 16, 32, 64):
         out.append((f"C4_floodmin_n256_f{f}", psync.FloodMin(f), 256, int(1_000_000 * s), {}, 8))
-    out.append(("C4_kset_n256_k2", psync.KSetAgreement(2), 256, int(200_000 * s), {}, 70))
+    for f in (0, 1, 2, 4, 8, 16, 32, 64):  # the same crash-stop sweep for KSet, R = 16
+        out.append((f"C4_kset_n256_k2_f{f}", psync.KSetAgreement(2), 256, int(200_000 * s),
+                    dict(schedule=H(drop_log2=0, good_round=0.0, crash_fmax=f)), 70))
     out.append(("C5_benor_n128", psync.BenOr(), 128, int(1_000_000 * s), {}, 11))
     # second-wave algorithms (not BASELINE configurations). B_alg by the
     # §8d recipe: (state read + written) + init. OTR2 = OTR; SLV (x, ts, vote, decision 4 B
@@ -110,6 +114,34 @@ def main():
         kern = rdist.allreduce_max(kns / args.steps / 1e9, device=f"cuda:{dev}")
         tot = rdist.allreduce_summary(last.summary, device=f"cuda:{dev}")
         R = g.cfg.rounds
+        split = None
+        names = alg.check_names
+        if spec is None and "SafetyPredicate" in names:
+            # a violation counts as a finding only while the Spec's safety predicate
+            # still held on the effective HO sets (first_fail[target] < first_fail[SafetyPredicate],
+            # as the adversary search scores it); the rest follow a predicate break. One extra,
+            # untimed launch with the per-instance summaries.
+            _, pi = g._ctx.run_batch_np(begin, I)
+            ff = pi["first_fail"].astype(np.int64)
+            sp = ff[:, names.index("SafetyPredicate")]
+            cnt = []
+            for k in alg.violation_slots:
+                if names[k] == "SafetyPredicate":
+                    continue
+                bad = ff[:, k] != 255
+                cnt += [int((bad & (ff[:, k] < sp)).sum()), int((bad & (ff[:, k] >= sp)).sum())]
+            cnt.append(int((sp != 255).sum()))
+            t = torch.tensor(cnt, dtype=torch.int64, device=f"cuda:{dev}")
+            if world > 1:
+                dist.all_reduce(t)
+            cnt = t.cpu().tolist()
+            split = {"instances_with_predicate_break": cnt[-1]}
+            j = 0
+            for k in alg.violation_slots:
+                if names[k] == "SafetyPredicate":
+                    continue
+                split[names[k]] = {"under_predicate": cnt[j], "after_predicate_break": cnt[j + 1]}
+                j += 2
         g.close()
         if rank == 0:
             pr_launch = I * n * R
@@ -136,6 +168,8 @@ def main():
                 "mean_termination_round": (sum(i * c for i, c in enumerate(th[:-1])) / done) if done else None,
                 "term_hist": th,
             }
+            if split is not None:
+                rec["violations_split"] = split
             results.append(rec)
             print(json.dumps(rec), flush=True)
     if rank == 0 and args.out:

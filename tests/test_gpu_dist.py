@@ -96,6 +96,7 @@ def test_bench_device_list_two_devices():
     """`bench.py --device-list 0,0` runs one context over two device slots
     (psg_config.devices), reports n_gpus = 2, and its node counters equal one context over
     the same 2 x I instances."""
+    from round_amd import psync
     per = 100_000
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device-list", "0,0", "--steps", "2", "--warmup", "1",
            "--instances", str(per), "--variants=", "--no-cpu-baseline"]

@@ -74,9 +74,10 @@ def test_c4_floodmin_f(f, oracle_mod):
         _check(gr, ids, oracle_mod)
 
 
-@pytest.mark.parametrize("f", [1, 64])
+@pytest.mark.parametrize("f", [1, 8, 32, 64])
 def test_c4_kset_f(f, oracle_mod):
-    """C4 KSet n=256 k=2 (the default crash-stop f < k, and the f = 64 end of the sweep)."""
+    """C4 KSet n=256 k=2 crash-stop sweep (bench_configs.py C4_kset_n256_k2_f*): the default
+    f < k, two inner points and the f = 64 end."""
     rng = random.Random(50 + f)
     ids = _ids(rng, 200_000, 24, extra=HIGH[:4])
     sched = psync.HOSchedule(drop_log2=0, good_round=0.0, crash_fmax=f)

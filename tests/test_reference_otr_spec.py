@@ -358,14 +358,14 @@ def test_lv_checker_matches_reference_formulas(n, count, sched, V, variant, orac
 # ------------------------------------------------------------------ the GPU checker, directly
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,variant", [(16, 0), (16, 1), (64, 0), (64, 1)])
-def test_gpu_first_fail_matches_reference_formulas(n, variant, oracle_mod):
+@pytest.mark.parametrize("n,variant,drop,V", [(16, 0, 2, 3), (7, 1, 2, 2), (16, 1, 2, 2), (64, 0, 2, 3), (64, 0, 3, 64)])
+def test_gpu_first_fail_matches_reference_formulas(n, variant, drop, V, oracle_mod):
     """The GPU's first failing check point of every exactly-determined slot equals the first
     check point where the reference formula fails, on the states of the same instances
     (trace from the oracle; the GPU's per-instance digests equal the oracle's)."""
     count = 400
     alg = psync.OTR(variant=variant)
-    cfg, tr, bits = _run(oracle_mod, n, 1 if variant else 2, 0.2, True, 2, variant, count=count)
+    cfg, tr, bits = _run(oracle_mod, n, drop, 0.2, True, 2, variant, count=count, V=V)
     data, decided, x, data0 = model_view(tr)
     data0 = np.broadcast_to(data0, data.shape)
     dec_valid = (~decided | (data[..., :, None] == data0[..., None, :]).any(-1)).all(-1)
@@ -378,8 +378,8 @@ def test_gpu_first_fail_matches_reference_formulas(n, variant, oracle_mod):
     def first_false(a):
         return np.where(a.all(-1), 255, np.argmin(a, axis=-1))
 
-    with psync.GpuRound(alg, n, rounds=R, seed=cfg.seed, value_range=3, batch_capacity=count,
-                        schedule=psync.HOSchedule(drop_log2=1 if variant else 2, good_round=0.2)) as g:
+    with psync.GpuRound(alg, n, rounds=R, seed=cfg.seed, value_range=V, batch_capacity=count,
+                        schedule=psync.HOSchedule(drop_log2=drop, good_round=0.2)) as g:
         assert g.cfg.seed == cfg.seed and g.cfg.param == cfg.param
         res = g.run(0, count, per_instance=True)
     ff = np.array([list(s.first_fail) for s in res.per_instance])
@@ -388,5 +388,7 @@ def test_gpu_first_fail_matches_reference_formulas(n, variant, oracle_mod):
         assert (ff[:, slot] == first_false(a)).all(), (slot, np.argwhere(ff[:, slot] != first_false(a))[:5])
     t = termination(decided)
     assert (term == np.where(t.any(-1), np.argmax(t, axis=-1), 255)).all()
+    osum, opi, _ = oracle_mod.run(cfg, 0, count, per_instance=True, threads=8)
+    assert [s.digest for s in res.per_instance] == [s.digest for s in opi]  # the same executions
     if variant:
-        assert (ff[:, AGREEMENT] != 255).any()
+        assert (ff[:, AGREEMENT] != 255).any() and (ff[:, IRREVOCABILITY] != 255).any()
