@@ -42,8 +42,10 @@
 #ifndef PSG_H
 #define PSG_H
 
+#ifndef __HIPCC_RTC__ /* hiprtc builds of the kernel sources define the integer types */
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {

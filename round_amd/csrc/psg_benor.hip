@@ -6,7 +6,9 @@
 // `util.Random.nextBoolean` (BenOr.scala:77) is java.util.Random's first
 // nextBoolean after setSeed(Philox(seed, instance, round, pid)).
 // n = 128 runs as W = 2 waves per instance with the ballot words exchanged in LDS.
+#ifndef __HIPCC_RTC__
 #include <type_traits>
+#endif
 
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"

@@ -8,8 +8,23 @@
 // popcounts and shuffles over those masks.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#else  // hiprtc (psg_spec_compile_native): the runtime is implicit, its integer types are namespaced
+using __hip_internal::int8_t;
+using __hip_internal::int16_t;
+using __hip_internal::int32_t;
+using __hip_internal::int64_t;
+using __hip_internal::uint8_t;
+using __hip_internal::uint16_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#define INT32_MIN (-2147483647 - 1)
+#define INT32_MAX 2147483647
+#define INT64_MIN (-9223372036854775807LL - 1)
+#define INT64_MAX 9223372036854775807LL
+#endif
 
 #include "../../include/psg.h"
 
@@ -415,6 +430,23 @@ PSG_DEV Mask<W> mfull(int n) {
   return m;
 }
 
+// A uniform value moved into a VGPR: the compiler treats the result as divergent, so the
+// arithmetic on it issues on the vector pipe. For the kernels bound by scalar issue (one SALU
+// instruction per cycle per CU, shared by every wave of the CU) against two VALU per cycle.
+PSG_DEV uint32_t vgpr_u32(uint32_t v) {
+  asm("; vgpr_u32" : "+v"(v));
+  return v;
+}
+// popcount of a mask on the vector pipe (v_bcnt), as a uniform value in a VGPR
+template <int W>
+PSG_DEV int mpopc_v(const Mask<W>& a) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < W; ++i)
+    c += (uint32_t)__builtin_popcount(vgpr_u32((uint32_t)a.w[i])) + (uint32_t)__builtin_popcount(vgpr_u32((uint32_t)(a.w[i] >> 32)));
+  return (int)c;
+}
+
 PSG_DEV uint64_t rfl64(uint64_t v) {
   uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
@@ -538,6 +570,8 @@ struct Grp {
     }
   }
   PSG_DEV bool any(bool pred) { return many(ballot(pred)); }
+  // any() for predicates that are false on every lane past n (no valid-lane mask)
+  PSG_DEV bool any_raw(bool pred) { return many(ballot_any(pred)); }
   // ballot() without the valid-lane mask (W == 1: one compare, no scalar AND); for
   // callers that only intersect the result with masks of valid processes
   PSG_DEV Mask<W> ballot_any(bool pred) {
@@ -981,29 +1015,20 @@ struct CrashSets {
 
 // ---------------------------------------------------------------- per-instance checks
 struct Checks {
-  // uniform bitmask of the slots that were false at some check point, plus one
-  // VGPR whose lane s (< PSG_MAX_CHECKS) holds slot s's first failing check
-  // point and lane PSG_MAX_CHECKS the termination check point.
-  uint32_t failed;
-  bool termed;
+  // One VGPR: lane s (< PSG_MAX_CHECKS) holds slot s's first failing check point, lane
+  // PSG_MAX_CHECKS the first check point where Termination holds (PSG_NEVER: none). Check
+  // points arrive in increasing order, so "first" is a running minimum, and recording is
+  // branch-free per-lane VALU work (no scalar state: the kernels are scalar-issue-bound).
   int32_t ffv;
-  PSG_DEV void reset() {
-    failed = 0;
-    termed = false;
-    ffv = PSG_NEVER;
-  }
-  // failbits: bit s set iff slot s is false at check point c (uniform)
+  PSG_DEV void reset() { ffv = PSG_NEVER; }
+  // failbits: bit s set iff slot s is false at check point c (uniform); term: Termination holds
   PSG_DEV void record(uint32_t failbits, bool term, int c, int lane) {
-    const uint32_t nf = failbits & ~failed;
-    if (nf) {
-      if (lane < PSG_MAX_CHECKS && ((nf >> lane) & 1u)) ffv = c;
-      failed |= nf;
-    }
-    if (term && !termed) {
-      if (lane == PSG_MAX_CHECKS) ffv = c;
-      termed = true;
-    }
+    const uint64_t bits = (uint64_t)(failbits | (term ? (1u << PSG_MAX_CHECKS) : 0u));
+    const int32_t at = ((bits >> lane) & 1ull) ? c : (int32_t)PSG_NEVER;  // lane < 64: a defined shift
+    ffv = at < ffv ? at : ffv;
   }
+  // slot `lane` (< PSG_MAX_CHECKS) failed at some check point
+  PSG_DEV bool failed_here() const { return ffv != (int32_t)PSG_NEVER; }
   PSG_DEV uint32_t term_round() const { return (uint32_t)__builtin_amdgcn_readlane(ffv, PSG_MAX_CHECKS); }
 };
 
@@ -1081,7 +1106,7 @@ PSG_DEV void finish_instance(Grp<W>& g, const KArgs& a, uint64_t i, const Checks
         *reinterpret_cast<uint16_t*>(o + 10 + PSG_MAX_CHECKS) = (uint16_t)nd;
       }
     }
-    if (g.lane < nchecks && ((ck.failed >> g.lane) & 1u)) atomicAdd(&bc->fail[g.lane], 1u);
+    if (g.lane < nchecks && ck.failed_here()) atomicAdd(&bc->fail[g.lane], 1u);
     if (g.lane == 0) {
       atomicAdd(&bc->hist[term == PSG_NEVER ? a.R + 1 : term], 1u);
       atomicAdd(&bc->decided, (unsigned int)nd);

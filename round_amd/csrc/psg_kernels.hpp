@@ -1,5 +1,6 @@
 // psg_kernels.hpp — launcher declarations (one translation unit per algorithm).
 #pragma once
+#ifndef __HIPCC_RTC__  // (a hiprtc build of a fused Spec module has no host launchers)
 #include <hip/hip_runtime.h>
 
 namespace psg {
@@ -34,3 +35,4 @@ hipError_t launch_spec_vm(const VmArgs& a, int grid, hipStream_t s);
 hipError_t launch_gen_init(uint64_t inst_begin, uint64_t count, int n, int alg, int V, uint64_t seed, int32_t* out,
                            hipStream_t s);
 }  // namespace psg
+#endif

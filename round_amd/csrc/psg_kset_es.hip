@@ -34,33 +34,44 @@ PSG_DEV void kset_es_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t
   sc.prep_good(0, P.lane, a.R);
   int32_t cr[W];
   pk_crash_rounds<W>(P, a, inst, cr);
-  // KSetESProcess state after init(io) (KSetEarlyStopping.scala:16-21)
-  int32_t est[W], lastNb[W], decision[W], dec_val[W], dec_round[W], halt_round[W];
-  uint32_t cd[W], decided[W], halted[W];
+  // KSetESProcess state after init(io) (KSetEarlyStopping.scala:16-21). Registers are what
+  // bounds this kernel (W mailboxes of W words each per lane), so the state is kept compact:
+  // a process decides and exits in the same round with decision = est, so the decide value
+  // is `decision`, the decide round is the halt round, and decided = halted on a process
+  // slot; canDecide and halted are bits j / 8 + j of one flag word.
+  int32_t est[W], decision[W];
+  uint32_t nbh[W];  // lastNb (bits 0..15) | halt round + 1 (bits 16..31: 0 = not halted)
+  uint32_t fl = 0;  // bit j: canDecide of slot j; bit 8 + j: slot j halted (or not a process)
 #pragma unroll
   for (int j = 0; j < W; ++j) {
     est[j] = 0;
     if (P.val[j])
       est[j] = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + P.pid(j)] : sc.init_value(P.pid(j), PSG_ALG_KSET_ES);
-    lastNb[j] = n;
-    decision[j] = dec_val[j] = 0;
-    dec_round[j] = halt_round[j] = -1;
-    cd[j] = decided[j] = 0;
-    halted[j] = 1u - P.val[j];
+    nbh[j] = (uint32_t)n;
+    decision[j] = 0;
+    fl |= (1u - P.val[j]) << (8 + j);
   }
   X0Set<W> X0;
   pk_x0_build<W>(P, X0, x0lds, est);
   Checks ck;
   ck.reset();
-  auto check = [&](int c) { pk_kagree_check<W>(P, ck, c, kk, decided, decision, cr, X0); };
+  auto check = [&](int c) {
+    uint32_t decided[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) decided[j] = P.val[j] & ((fl >> (8 + j)) & 1u);
+    pk_kagree_check<W>(P, ck, c, kk, decided, decision, cr, X0);
+  };
   check(0);
   for (int k = 0; k < a.R; ++k) {
-    uint32_t al[W];
+    uint32_t al[W], cdw[W];
 #pragma unroll
-    for (int j = 0; j < W; ++j) al[j] = 1u - halted[j];
+    for (int j = 0; j < W; ++j) {
+      al[j] = 1u - ((fl >> (8 + j)) & 1u);
+      cdw[j] = (fl >> j) & 1u;
+    }
     const Mask<W> act = P.ballot(al);  // alive senders
     if (many(act)) {
-      const Mask<W> CD = P.ballot(cd);  // senders' canDecide flags (pre-state)
+      const Mask<W> CD = P.ballot(cdw);  // senders' canDecide flags (pre-state)
       Mask<W> goodS;
       const bool good = sc.good_round(k, P.lane, a.R, goodS);
       Mask<W> CB = mzero<W>(), CN = mzero<W>();
@@ -71,31 +82,62 @@ PSG_DEV void kset_es_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t
           CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
         }
       }
-      Mask<W> M[W];
-      int32_t currNb[W], nest[W];
-      uint32_t anyCD[W], decideNow[W], unres[W], selfIn[W];
+      // The distinct sender estimates are visited in ascending order (the first step's value
+      // is the minimum over every alive sender, known before any mailbox); each receiver
+      // resolves at the first value whose senders meet its mailbox. A receiver's mailbox
+      // (W words) is formed, used for the first step and dropped: the rare receivers still
+      // unresolved after it re-form theirs at each later step (Sched::ho is a pure function
+      // of (k, pid); with crash-stop HO sets it draws only in the crash rounds), so no W x W
+      // words of mailboxes stay live in registers (they spilled to scratch).
+      int32_t mn = INT32_MAX;
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+        if ((act.w[j] >> P.lane) & 1ull) mn = min(mn, est[j]);
+      const int32_t v1 = Grp<1>::dpp_reduce32<false>(mn);  // act non-empty: a sender value
+      uint32_t eq1[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) eq1[j] = eq01(est[j], v1);
+      const Mask<W> E1 = mand(P.ballot(eq1), act);
+      int32_t nest[W];
+      uint32_t unres = 0, selfIn = 0, dnow = 0;  // bit j per slot
 #pragma unroll
       for (int j = 0; j < W; ++j) {
-        M[j] = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
-        currNb[j] = mpopc(M[j]);
-        anyCD[j] = many(mand(M[j], CD)) ? 1u : 0u;  // mailbox.exists(_._2._2), pre-update flags
-        decideNow[j] = (1u - halted[j]) & ((k > t / kk) ? 1u : cd[j]);
-        // est = min over the mailbox's estimates (unchanged if the mailbox is empty)
-        unres[j] = (1u - halted[j]) & (1u - decideNow[j]) & (currNb[j] > 0 ? 1u : 0u);
-        selfIn[j] = (uint32_t)((M[j].w[j] >> P.lane) & 1ull);
+        const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
+        const int32_t currNb = mpopc(M);
+        const uint32_t live = 1u - ((fl >> (8 + j)) & 1u);
+        const uint32_t cd = (fl >> j) & 1u;
+        const uint32_t decideNow = live & ((k > t / kk) ? 1u : cd);
+        const uint32_t self = (uint32_t)((M.w[j] >> P.lane) & 1ull);
         nest[j] = est[j];
-      }
-      Mask<W> rem = act;
-      while (many(rem)) {
-        int32_t mn = INT32_MAX;
-        uint32_t anyU = 0;
-#pragma unroll
-        for (int j = 0; j < W; ++j) {
-          if ((rem.w[j] >> P.lane) & 1ull) mn = min(mn, est[j]);
-          anyU |= unres[j];
+        // est = min over the mailbox's estimates (unchanged if the mailbox is empty)
+        uint32_t u = live & (1u - decideNow) & (currNb > 0 ? 1u : 0u);
+        if (u) {
+          if (many(mand(M, E1))) {
+            nest[j] = v1;
+            u = 0;
+          } else if (self && v1 >= est[j]) {
+            u = 0;  // nothing below the receiver's own estimate reached it
+          }
         }
-        if (!pk_any(anyU)) break;
-        const int32_t v = Grp<1>::dpp_reduce32<false>(mn);  // rem non-empty: a sender value
+        unres |= u << j;
+        selfIn |= self << j;
+        dnow |= decideNow << j;
+        if (live && !decideNow) {  // KSetEarlyStopping.scala:36-38 (variant 1: mutation, always canDecide)
+          const bool anyCD = many(mand(M, CD));  // mailbox.exists(_._2._2), pre-update flags
+          const int32_t lastNb = (int32_t)(nbh[j] & 0xFFFFu);
+          const uint32_t ncd = a.variant == 1 ? 1u : ((anyCD || lastNb - currNb < kk) ? 1u : 0u);
+          fl = (fl & ~(1u << j)) | (ncd << j);
+          nbh[j] = (nbh[j] & 0xFFFF0000u) | (uint32_t)currNb;
+        }
+      }
+      Mask<W> rem = mandn(act, E1);
+      while (many(rem)) {
+        if (!pk_any(unres)) break;
+        int32_t mv = INT32_MAX;
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+          if ((rem.w[j] >> P.lane) & 1ull) mv = min(mv, est[j]);
+        const int32_t v = Grp<1>::dpp_reduce32<false>(mv);  // rem non-empty: a sender value
         uint32_t eq[W];
 #pragma unroll
         for (int j = 0; j < W; ++j) eq[j] = eq01(est[j], v);
@@ -103,39 +145,38 @@ PSG_DEV void kset_es_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t
         rem = mandn(rem, E);
 #pragma unroll
         for (int j = 0; j < W; ++j) {
-          if (unres[j]) {
-            if (many(mand(M[j], E))) {
+          if ((unres >> j) & 1u) {
+            const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
+            if (many(mand(M, E))) {
               nest[j] = v;
-              unres[j] = 0;
-            } else if (selfIn[j] && v >= est[j]) {
-              unres[j] = 0;  // nothing below the receiver's own estimate reached it
+              unres &= ~(1u << j);
+            } else if (((selfIn >> j) & 1u) && v >= est[j]) {
+              unres &= ~(1u << j);  // nothing below the receiver's own estimate reached it
             }
           }
         }
       }
 #pragma unroll
       for (int j = 0; j < W; ++j) {
-        if (decideNow[j]) {  // callback.decide(est); exitAtEndOfRound (KSetEarlyStopping.scala:32-34)
-          dec_val[j] = est[j];
-          dec_round[j] = k;
-          decided[j] = 1;
+        if ((dnow >> j) & 1u) {  // callback.decide(est); exitAtEndOfRound (KSetEarlyStopping.scala:32-34)
           decision[j] = est[j];
-          halt_round[j] = k;
-          halted[j] = 1;
-        } else if (!halted[j]) {  // KSetEarlyStopping.scala:36-38 (variant 1: mutation, always canDecide)
+          nbh[j] = (nbh[j] & 0xFFFFu) | ((uint32_t)(k + 1) << 16);
+          fl |= 1u << (8 + j);
+        } else if (!((fl >> (8 + j)) & 1u)) {
           est[j] = nest[j];
-          cd[j] = a.variant == 1 ? 1u : ((anyCD[j] || lastNb[j] - currNb[j] < kk) ? 1u : 0u);
-          lastNb[j] = currNb[j];
         }
       }
     }
     check(k + 1);
   }
-  pk_finish<W>(P, a, i, ck, 2, dec_val, dec_round, halt_round, est, bc);
+  int32_t halt_round[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) halt_round[j] = (int32_t)(nbh[j] >> 16) - 1;
+  pk_finish<W>(P, a, i, ck, 2, decision, halt_round, halt_round, est, bc);
 }
 
 #ifndef PSG_KSETES_PK_WPE
-#define PSG_KSETES_PK_WPE 5  // W = 4: 5 waves/SIMD (with some scratch) measured over 3 / 4: 17.2 vs 18.5 / 17.9 ms
+#define PSG_KSETES_PK_WPE 4  // W = 4, compact state (no scratch): 4 waves/SIMD 15.7 ms vs 5 (156 B scratch) 16.7 ms
 #endif
 template <int W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_KSETES_PK_WPE)))

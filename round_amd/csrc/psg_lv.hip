@@ -7,11 +7,16 @@
 // maxBy over the R0 mailbox (LastVoting.scala:132) takes the first max in Scala
 // Map iteration order: insertion order (ascending pid) up to 4 entries, CHAMP
 // order beyond, computed from per-lane CHAMP sort keys and a wave min-reduction.
+#ifndef __HIPCC_RTC__
 #include <type_traits>
+#endif
 
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
 
+#ifndef PSG_LV_CHECK_V2
+#define PSG_LV_CHECK_V2 1
+#endif
 #ifndef PSG_LV_EXP
 #define PSG_LV_EXP 0  // timing experiments only (1: no majority scan, 2: check reduced to termination)
 #endif
@@ -47,12 +52,77 @@ PSG_DEV void lv_stage(Grp<W>& g, LvLds<W>& L, int32_t x, int32_t ts, int32_t vot
 // xin01 / din01: 1 iff x / decision is an initial value (tracked by the round step: x and
 // decision only ever take the coordinator's uniform vote, whose membership is probed once).
 template <int W>
-PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, bool has_old, int n, const Mask<W>& full,
-                      int32_t x, int32_t ts, int32_t vote, int32_t decision, uint32_t fl, uint32_t old_fl,
-                      int32_t old_decision, uint32_t xin01, uint32_t din01) {
+PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, int32_t r4, int coord, bool has_old, int n,
+                      const Mask<W>& full, int32_t x, int32_t ts, int32_t vote, int32_t decision, uint32_t fl,
+                      uint32_t old_fl, int32_t old_decision, uint32_t xin01, uint32_t din01) {
+  // r4 = c / 4, coord = (c / 4) % n: maintained incrementally by the caller (a runtime `% n`
+  // is a scalar multiply-high sequence per use on this scalar-issue-bound kernel)
   lv_stage<W>(g, L, x, ts, vote, decision);
-  const int32_t r4 = c / 4;
-  const int coord = r4 % n;
+#if PSG_LV_CHECK_V2
+  // Scalar-lean form: the kernel is bound by scalar issue (SALU 0.94 of one per cycle per CU),
+  // so every "some process" test is one ballot of a per-lane VALU predicate, and the
+  // binary search's bookkeeping runs in uniform VGPRs; the formulas are those of the
+  // reference form below (kept for A/B: -DPSG_LV_CHECK_V2=0).
+  const uint32_t dec01 = fl & F_DECIDED;  // F_DECIDED == 1
+  const Mask<W> D = g.ballot(dec01 != 0u);
+  const bool anyD = many(D);
+  const int32_t d0 = anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
+  if (PSG_LV_EXP == 2) { ck.record(0, meq(D, full), c, g.lane); return; }
+  // Agreement, keepInit, Validity and Irrevocability from one ballot of a per-process
+  // witness word (decision != d0; x or a decision not initial; a changed decision),
+  // resolved formula by formula only when some process is a witness
+  uint32_t wit = (dec01 & (ne01(decision, d0) | (1u - din01))) | (1u - xin01);
+  if (has_old) wit |= (old_fl & F_DECIDED) & (1u - (dec01 & eq01(old_decision, decision)));
+  bool same = true, keep = true, validity = true, irrev = true;
+  if (g.any_raw(wit != 0u)) {  // wit, dec01, old_fl & F_DECIDED are 0 past n
+    same = !g.any_raw(dec01 != 0u && decision != d0);
+    keep = !g.any(xin01 == 0u);  // P.forall(i => P.exists(j1 => i.x == init(j1.x)))
+    validity = !g.any_raw(dec01 != 0u && din01 == 0u);
+    irrev = !has_old || !g.any_raw((old_fl & F_DECIDED) != 0u && !(dec01 != 0u && old_decision == decision));
+  }
+  const bool noDec = !g.any_raw((fl & (F_DECIDED | F_READY)) != 0u);  // flags are 0 past n but F_HALTED
+  // values pinned by (decided ==> decision == v), (commit ==> vote == v), (ready ==> vote == v):
+  // z0 = the pinned value of the first pinned process (its decision if it decided, else its
+  // vote), and every pinned process must agree with it
+  const uint32_t cr01 = (fl & (F_COMMIT | F_READY)) ? 1u : 0u;
+  const Mask<W> Pm = g.ballot_any((dec01 | cr01) != 0u);
+  const bool zAny = many(Pm);
+  int32_t z0 = 0;
+  bool zOk = true;
+  if (zAny) {
+    const int32_t zl = dec01 ? decision : vote;
+    if constexpr (W > 1) {
+      L.votes[g.pid] = zl;  // the staged votes are not read after this point of the check
+      __syncthreads();
+    }
+    z0 = g.bcast(zl, L.votes, mfirst(Pm));
+    zOk = !g.any_raw(((dec01 & ne01(decision, z0)) | (cr01 & ne01(vote, z0))) != 0u);
+  }
+  bool maj = false;
+  // (Invariant0 reads maj only when keepInit holds and some process decided or is ready)
+  if (PSG_LV_EXP != 1 && c > 0 && zOk && keep && !noDec &&
+      // (i.ts == r/4) ==> coord.commit
+      (mtest(g.ballot_any((fl & F_COMMIT) != 0u), coord) || !g.any_raw(ts == r4))) {  // ts = -1 past n
+    // exists t <= r/4: A_t = {i : i.ts >= t}, |A_t| > n/2, all x over A_t equal (to the pinned
+    // value): the largest u with |{tv >= u}| > n/2 for tv = min(ts, r/4) + 1 (see below), by
+    // binary search; ceil(log2(r/4 + 2)) = bit length of r/4 + 1 steps (a step after
+    // convergence keeps lo), lo / hi / mid as uniform VGPR values (vector issue)
+    const int32_t tsc = ts < r4 ? ts : r4;
+    const uint32_t tv = (uint32_t)(tsc + 1);  // ts >= -1 (LastVoting.scala:87)
+    const int steps = 32 - __builtin_clz((uint32_t)r4 + 1u);
+    uint32_t lo = vgpr_u32(0u), hi = vgpr_u32((uint32_t)r4 + 2u);
+    const uint32_t half = (uint32_t)(n / 2);
+    for (int s = 0; s < steps; ++s) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const bool ok = (uint32_t)mpopc_v(g.ballot_any(tv >= mid)) > half;  // tv = 0 past n, mid >= 1
+      lo = ok ? mid : lo;
+      hi = ok ? hi : mid;
+    }
+    const Mask<W> A = g.ballot(tv >= lo);
+    const int32_t xv = g.bcast(x, L.xs, mfirst(A));
+    maj = !g.any(tv >= lo && x != xv) && (!zAny || xv == z0);
+  }
+#else
   const uint32_t dec01 = (fl & F_DECIDED) ? 1u : 0u;
   const Mask<W> D = g.ballot(dec01 != 0u);
   const Mask<W> C = g.ballot((fl & F_COMMIT) != 0u);
@@ -110,6 +180,7 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, bool has_old, i
     const int32_t xv = g.bcast(x, L.xs, mfirst(A));
     maj = !many(mand(A, g.ballot(x != xv))) && (!zAny || xv == z0);
   }
+#endif
   const bool inv0 = keep && (noDec || maj);
   const bool d0in = same && validity;
   const bool term = meq(D, full);
@@ -215,7 +286,7 @@ PSG_DEV void lv_body(const KArgs& a) {
     Checks ck;
     ck.reset();
     typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
-    if constexpr (!SH::kFused) lv_check<W>(g, L, ck, 0, false, n, full, x, ts, vote, decision, fl, 0u, -1, xin, din);
+    if constexpr (!SH::kFused) lv_check<W>(g, L, ck, 0, 0, 0, false, n, full, x, ts, vote, decision, fl, 0u, -1, xin, din);
     auto trace = [&](int c, int32_t hs) {
       emit_state<W, SH>(sh, g, a, i, c, x, (fl & F_DECIDED) ? 1 : 0, decision, ts, (fl & F_READY) ? 1 : 0,
                    (fl & F_COMMIT) ? 1 : 0, vote, 0, hs);
@@ -224,6 +295,9 @@ PSG_DEV void lv_body(const KArgs& a) {
     pt.mark(0);
 
     // one round of slot RS = k mod 4 (compile time: each slot's step and check specialized)
+    // phase = k / 4 and its coordinator (phase % n), and the next phase's, kept incrementally
+    int32_t phase = 0;
+    int cph = 0, cnx = n > 1 ? 1 : 0;
     auto round = [&](const int k, auto RSc) {
       constexpr int RS = decltype(RSc)::value;
       const uint32_t old_fl = fl;
@@ -231,8 +305,7 @@ PSG_DEV void lv_body(const KArgs& a) {
       const Mask<W> act = g.ballot((fl & F_HALTED) == 0u);
       int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
-        const int32_t phase = k >> 2;
-        const int c = phase % n;
+        const int c = cph;
         const bool cAlive = mtest(act, c);
         const uint32_t live = (fl & F_HALTED) ? 0u : 1u;
         Mask<W> goodS;
@@ -307,7 +380,9 @@ PSG_DEV void lv_body(const KArgs& a) {
         }
         pt.mark(2);
       }
-      if constexpr (!SH::kFused) lv_check<W>(g, L, ck, k + 1, true, n, full, x, ts, vote, decision, fl, old_fl, old_decision, xin, din);
+      if constexpr (!SH::kFused)
+        lv_check<W>(g, L, ck, k + 1, RS == 3 ? phase + 1 : phase, RS == 3 ? cnx : cph, true, n, full, x, ts, vote,
+                    decision, fl, old_fl, old_decision, xin, din);
       if (tracing<SH>(a)) trace(k + 1, (old_fl & F_HALTED) ? n : hs);
       pt.mark(many(act) ? 4 : 5);
     };
@@ -316,6 +391,9 @@ PSG_DEV void lv_body(const KArgs& a) {
       if (k0 + 1 < a.R) round(k0 + 1, std::integral_constant<int, 1>{});
       if (k0 + 2 < a.R) round(k0 + 2, std::integral_constant<int, 2>{});
       if (k0 + 3 < a.R) round(k0 + 3, std::integral_constant<int, 3>{});
+      ++phase;
+      cph = cnx;
+      cnx = cnx + 1 == n ? 0 : cnx + 1;
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 7, dec_val, dec_round, halt_round, x, &bc);
     pt.mark(3);

@@ -185,7 +185,7 @@ PSG_DEV void pk_finish(const Pk<W>& P, const KArgs& a, uint64_t i, const Checks&
       *reinterpret_cast<uint16_t*>(o + 10 + PSG_MAX_CHECKS) = (uint16_t)nd;
     }
   }
-  if (P.lane < nchecks && ((ck.failed >> P.lane) & 1u)) atomicAdd(&bc->fail[P.lane], 1u);
+  if (P.lane < nchecks && ck.failed_here()) atomicAdd(&bc->fail[P.lane], 1u);
   if (P.lane == 0) {
     atomicAdd(&bc->hist[term == PSG_NEVER ? a.R + 1 : term], 1u);
     atomicAdd(&bc->decided, nd);

@@ -19,7 +19,9 @@
 // Map order by psg_selftest_map_head.
 // Spec: TrivialSpec; the build checks uniform agreement (k = 1 over every
 // decider, HO-model consensus) and validity.
+#ifndef __HIPCC_RTC__
 #include <type_traits>
+#endif
 
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"

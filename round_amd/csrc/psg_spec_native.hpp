@@ -493,7 +493,7 @@ __device__ void native_kernel_body(const VmArgs& A) {
           o[9 + PSG_MAX_CHECKS] = (uint8_t)S::kSlots;
         }
       }
-      if (g.lane < S::kSlots && ((ck.failed >> g.lane) & 1u)) atomicAdd(&bc.fail[g.lane], 1u);
+      if (g.lane < S::kSlots && ck.failed_here()) atomicAdd(&bc.fail[g.lane], 1u);
       if (g.lane == 0) atomicAdd(&bc.hist[term == PSG_NEVER ? A.R + 1 : term], 1u);
     }
   }
