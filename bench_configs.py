@@ -67,6 +67,13 @@ def configs(scale):
                 lambda: formula.compile_native(formula.otr_spec(), abi.PSG_ALG_OTR, fused=True, n=64)))
     out.append(("G1_lv_n64_fused", psync.LastVoting(), 64, int(12_500_000 * s), {}, 42,
                 lambda: formula.compile_native(formula.lv_spec(), abi.PSG_ALG_LAST_VOTING, fused=True, n=64)))
+    # ... and the same Specs given as Formula text, lowered by the library itself
+    # (psg_spec_compile_native: the JVM plugin's route, GpuSpec.compile(native = true))
+    from round_amd import lib
+    out.append(("G1_otr_n64_fused_text", psync.OTR(), 64, int(10_000_000 * s), dict(value_range=64), 24,
+                lambda: lib.spec_compile_native(formula.to_text(formula.otr_spec()), abi.PSG_ALG_OTR, True, 64)))
+    out.append(("G1_lv_n64_fused_text", psync.LastVoting(), 64, int(12_500_000 * s), {}, 42,
+                lambda: lib.spec_compile_native(formula.to_text(formula.lv_spec()), abi.PSG_ALG_LAST_VOTING, True, 64)))
     return out
 
 

@@ -315,6 +315,27 @@ int psg_spec_from_text(const char* text, int32_t alg, psg_spec_program* out, cha
                        char* err, size_t err_len);
 void psg_spec_release(psg_spec_program* prog);
 
+/* Native lowering of Formula text, in-process (the C-ABI / JVM route to what
+ * round_amd/formula.py compile_native builds from Python; replaces, for concrete checking, the
+ * Verifier's lowering of a psync.Spec, psync/Specs.scala:8-16, psync/formula/Formula.scala:5-585).
+ * The program is psg_spec_from_text's; out->module_path names a gfx950 code object generated
+ * from the same Formula tree (equality pins, count guards, breakpoint finitization, tuple
+ * quantifiers, memoized init membership, hoisted common subformulas) and compiled with hiprtc,
+ * cached by a hash of its source and the kernel headers in cache_dir (NULL: <library
+ * dir>/../build/spec, shared with formula.compile_native). fused != 0: the module also holds
+ * the algorithm's round kernel with the Spec as its check hook, so psg_run_batch_spec runs one
+ * launch; n > 0 limits its instantiations to that group size. The path string is the library's
+ * (valid until the process exits); release the arrays with psg_spec_release. Kernel sources
+ * are read from <library dir>/csrc and <library dir>/../include (PSG_CSRC / PSG_INCLUDE
+ * override). No device needed to compile. */
+int psg_spec_compile_native(const char* text, int32_t alg, int32_t fused, int32_t n, const char* cache_dir,
+                            psg_spec_program* out, char* names, size_t names_len, char* err, size_t err_len);
+/* The HIP source psg_spec_compile_native compiles for these arguments (tests, inspection):
+ * *src_len = capacity in, the size needed (with the terminating NUL) out; PSG_ERANGE when
+ * src is NULL or too small. */
+int psg_spec_native_source(const char* text, int32_t alg, int32_t fused, int32_t n, char* src, size_t* src_len,
+                           char* err, size_t err_len);
+
 /* Real-valued algorithms (PSG_ALG_EPSILON, RealConsensusIO, Epsilon.scala:10-13).
  * Same contracts as the int32 entry points; other algorithms get PSG_EINVAL.
  * host_init: [count][n] Double initial values, NULL = seeded (uniform [0,1)). */

@@ -323,6 +323,32 @@ JNIEXPORT jstring JNICALL Java_psync_gpu_GpuRoundNative_00024_compileSpecNames(J
   return out;
 }
 
+/* String compileSpecNative(String text, int alg, boolean fused, int n) — psg_spec_compile_native:
+ * the Spec's Formula text lowered to gfx950 code in the library (hiprtc, cached; fused: with the
+ * algorithm's round kernel), returned as the code object's path for runBatchSpec's modulePath
+ * (the program itself is compileSpec's). */
+JNIEXPORT jstring JNICALL Java_psync_gpu_GpuRoundNative_00024_compileSpecNative(JNIEnv* env, jobject self,
+                                                                                jstring text, jint alg,
+                                                                                jboolean fused, jint n) {
+  (void)self;
+  if (!text) {
+    throw_cls(env, "java/lang/IllegalArgumentException", "text must not be null");
+    return NULL;
+  }
+  const char* t = (*env)->GetStringUTFChars(env, text, NULL);
+  psg_spec_program p;
+  char err[4096];
+  const int rc = psg_spec_compile_native(t, alg, fused ? 1 : 0, n, NULL, &p, NULL, 0, err, sizeof err);
+  (*env)->ReleaseStringUTFChars(env, text, t);
+  if (rc) {
+    throw_psg(env, rc, err);
+    return NULL;
+  }
+  jstring out = (*env)->NewStringUTF(env, p.module_path);
+  psg_spec_release(&p);
+  return out;
+}
+
 /* void copyDecisions(long ctx, int[] decision, int[] decisionRound) — the batched
  * ConsensusIO.decide results of the last batch, [count][n] each (either may be null). */
 JNIEXPORT void JNICALL Java_psync_gpu_GpuRoundNative_00024_copyDecisions(JNIEnv* env, jobject self, jlong h,

@@ -31,6 +31,7 @@ object GpuRoundNative {
   @native def copyDecisions(ctx: Long, decision: Array[Int], decisionRound: Array[Int]): Unit
   @native def compileSpec(text: String, alg: Int): Array[Int]
   @native def compileSpecNames(text: String, alg: Int): String
+  @native def compileSpecNative(text: String, alg: Int, fused: Boolean, n: Int): String
   @native def fetch(ctx: Long, ids: Array[Long], sums: Array[Byte], records: Array[Int]): Unit
   @native def loadSchedule(ctx: Long, begin: Long, count: Long, ho: Array[Long], crash: Array[Int]): Unit
   @native def clearSchedule(ctx: Long): Unit

@@ -93,13 +93,18 @@ object GpuSpec {
     sb.toString
   }
 
-  /** Compile `alg`'s own Spec (or any other of its Specs) for psg_run_batch_spec. */
-  def compile(alg: Algorithm[_, _], spec: Algorithm[_, _]#Spec): Program = {
+  /** Compile `alg`'s own Spec (or any other of its Specs) for psg_run_batch_spec. `native`:
+    * also lower it to gfx950 code in the library (psg_spec_compile_native, hiprtc, cached);
+    * `fused` (with native): one launch that runs the rounds and checks the Spec from
+    * registers; `n`: the group size the module is instantiated for (0: every size). */
+  def compile(alg: Algorithm[_, _], spec: Algorithm[_, _]#Spec, native: Boolean = false, fused: Boolean = false,
+              n: Int = 0): Program = {
     val id = GpuRound.algId(alg)
     val t = text(spec, phaseLength.getOrElse(id, 1))
     val packed = GpuRoundNative.compileSpec(t, id)
     val (ns, nw) = (packed(0), packed(1))
+    val module = if (native || fused) GpuRoundNative.compileSpecNative(t, id, fused, n) else null
     Program(packed.slice(4, 4 + nw), packed.slice(4 + nw, 4 + nw + ns), packed.slice(4 + nw + ns, 4 + nw + 2 * ns),
-            packed(2), packed(3), id, GpuRoundNative.compileSpecNames(t, id).split("\n"))
+            packed(2), packed(3), id, GpuRoundNative.compileSpecNames(t, id).split("\n"), module)
   }
 }

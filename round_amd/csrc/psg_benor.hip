@@ -291,7 +291,7 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
       if (sc.crash_on) {
 #pragma unroll
         for (int j = 0; j < W; ++j) {
-          CB.w[j] = __builtin_amdgcn_ballot_w64(cr[j] >= 0 && cr[j] < k);
+          CB.w[j] = __builtin_amdgcn_ballot_w64((uint32_t)cr[j] < (uint32_t)k);
           CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
         }
       }

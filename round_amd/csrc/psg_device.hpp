@@ -898,6 +898,7 @@ struct Sched {
   }
 
   PSG_DEV bool good_round(int k, int lane, int R, Mask<W>& s) {
+    if (good_p32 == 0) return false;  // no good rounds in this launch (one scalar test per round)
     if (k - good_base >= 64) prep_good(k, lane, R);
     const int off = k - good_base;
     const bool good = (good_mask >> off) & 1ull;
@@ -1000,13 +1001,14 @@ struct CrashSets {
     }
   }
   PSG_DEV void sets(Grp<W>& g, int k, Mask<W>& CB, Mask<W>& CN) const {
+    // crashed before round k: 0 <= cr < k, one unsigned compare (cr = -1: correct)
     if constexpr (W == 1) {
-      CB = g.ballot(cr[0] >= 0 && cr[0] < k);
+      CB = g.ballot((uint32_t)cr[0] < (uint32_t)k);
       CN = g.ballot(cr[0] == k);
     } else {
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        CB.w[w] = __builtin_amdgcn_ballot_w64(cr[w] >= 0 && cr[w] < k);
+        CB.w[w] = __builtin_amdgcn_ballot_w64((uint32_t)cr[w] < (uint32_t)k);
         CN.w[w] = __builtin_amdgcn_ballot_w64(cr[w] == k);
       }
     }

@@ -22,12 +22,10 @@
 #include <vector>
 
 #include "../../include/psg.h"
+#include "psg_spec_ir.hpp"
 
+namespace psgspec {
 namespace {
-
-struct SpecError : std::runtime_error {
-  using std::runtime_error::runtime_error;
-};
 
 // ------------------------------------------------------------------ S-expressions
 struct Sx {
@@ -86,69 +84,6 @@ struct Reader {
     s.tok.assign(p, q);
     p = q;
     return s;
-  }
-};
-
-// ------------------------------------------------------------------ expression IR (= formula.py Expr)
-enum Kind { LIT, NV, RV, COORDV, VAR, FIELD, UN, BIN, QUANT, CONTAINS };
-enum QK { QFORALL, QEXISTS, QCOUNT, QVINT, QVBOOL };
-struct Node {
-  Kind k;
-  int32_t v = 0;       // LIT value
-  int op = 0;          // UN / BIN opcode (enum psg_op)
-  int f = 0, tag = 0;  // FIELD
-  int uid = -1;        // VAR uid; QUANT / CONTAINS bound variable uid
-  int qk = 0;          // QUANT kind
-  int a = -1, b = -1;  // children: FIELD proc=a; UN x=a; BIN x=a y=b; QUANT body=a; CONTAINS elem=a, set body=b
-};
-struct Comp {  // a set of processes {var. body}
-  int var, body;
-};
-
-struct Tree {
-  std::vector<Node> nodes;
-  int next_uid = 0;
-  int add(Node n) {
-    nodes.push_back(n);
-    return (int)nodes.size() - 1;
-  }
-  int lit(int32_t v) { Node n{LIT}; n.v = v; return add(n); }
-  int bin(int op, int x, int y) { Node n{BIN}; n.op = op; n.a = x; n.b = y; return add(n); }
-  int un(int op, int x) { Node n{UN}; n.op = op; n.a = x; return add(n); }
-  int quant(int kind, int var, int body) { Node n{QUANT}; n.qk = kind; n.uid = var; n.a = body; return add(n); }
-  int var(int uid) { Node n{VAR}; n.uid = uid; return add(n); }
-  // children in formula.py's Expr.children() order
-  void children(int e, std::vector<int>& out) const {
-    const Node& n = nodes[e];
-    switch (n.k) {
-      case FIELD: case UN: case QUANT: out.push_back(n.a); break;
-      case BIN: case CONTAINS: out.push_back(n.a); out.push_back(n.b); break;
-      default: break;
-    }
-  }
-  void walk(int e, std::vector<int>& out) const {  // pre-order (formula.py _walk)
-    out.push_back(e);
-    std::vector<int> ch;
-    children(e, ch);
-    for (int c : ch) walk(c, out);
-  }
-  void free_vars(int e, std::set<int>& bound, std::set<int>& out) const {
-    const Node& n = nodes[e];
-    if (n.k == VAR) {
-      if (!bound.count(n.uid)) out.insert(n.uid);
-      return;
-    }
-    if (n.k == QUANT || n.k == CONTAINS) {
-      if (n.k == CONTAINS) free_vars(n.a, bound, out);
-      const int body = n.k == QUANT ? n.a : n.b;
-      const bool added = bound.insert(n.uid).second;
-      free_vars(body, bound, out);
-      if (added) bound.erase(n.uid);
-      return;
-    }
-    std::vector<int> ch;
-    children(e, ch);
-    for (int c : ch) free_vars(c, bound, out);
   }
 };
 
@@ -354,6 +289,8 @@ int32_t word(int op, int a = 0, int b = 0) {
   return (int32_t)((uint32_t)(op & 0xFF) | ((uint32_t)(a & 0xFF) << 8) | ((uint32_t)(b & 0xFFFF) << 16));
 }
 
+}  // namespace
+
 std::set<int> alg_fields(int alg) {
   using S = std::set<int>;
   switch (alg) {
@@ -371,6 +308,56 @@ std::set<int> alg_fields(int alg) {
   }
   throw SpecError("algorithm " + std::to_string(alg) + " has no integer state to check");
 }
+
+// (= formula.py _Compiler.witnesses)
+void witnesses(const Tree& T, int e, std::vector<int>& exprs, std::vector<std::pair<int, int>>& fsets) {
+  const Node& q = T.nodes[e];
+  const int v = q.uid;
+  std::vector<int> w;
+  T.walk(q.a, w);
+  std::set<int> inner;
+  for (int x : w)
+    if (T.nodes[x].k == QUANT || T.nodes[x].k == CONTAINS) inner.insert(T.nodes[x].uid);
+  bool seen = false;
+  for (int x : w) {
+    const Node& b = T.nodes[x];
+    if (b.k != BIN || b.op < PSG_OP_EQ || b.op > PSG_OP_GE) continue;
+    const int pairs[2][2] = {{b.a, b.b}, {b.b, b.a}};
+    for (auto& pr : pairs) {
+      const Node& a = T.nodes[pr[0]];
+      if (a.k != VAR || a.uid != v) continue;
+      std::set<int> bound, fv;
+      T.free_vars(pr[1], bound, fv);
+      if (fv.count(v)) throw SpecError("V.exists variable compared with a term containing itself");
+      const Node& t = T.nodes[pr[1]];
+      if (t.k == FIELD) {
+        const std::pair<int, int> key{t.f, t.tag};
+        bool have = false;
+        for (auto& k : fsets) have = have || k == key;
+        if (!have) fsets.push_back(key);
+      } else {
+        bool dep = false;
+        for (int u : fv) dep = dep || inner.count(u);
+        if (dep) throw SpecError("V.exists witness term depends on an inner bound variable and is not a process field");
+        exprs.push_back(pr[1]);
+      }
+      seen = true;
+    }
+  }
+  for (int x : w)
+    if (T.nodes[x].k == VAR && T.nodes[x].uid == v && !seen)
+      throw SpecError("a V.exists variable may only appear directly in comparisons");
+}
+
+bool uses_old(const Tree& T, int e) {
+  std::vector<int> w;
+  T.walk(e, w);
+  for (int x : w)
+    if (T.nodes[x].k == FIELD && T.nodes[x].tag == PSG_TAG_OLD) return true;
+  return false;
+}
+
+namespace {
 
 struct Compiler {
   const Tree& T;
@@ -449,7 +436,7 @@ struct Compiler {
     } else if (q.qk == QVBOOL) {
       head = word(PSG_OP_QBEGIN, PSG_Q_EXISTS_VB, slot);
     } else {
-      witnesses(e, exprs, fsets);
+      witnesses(T, e, exprs, fsets);
       for (int t : exprs) expr(t, depth, in_lane);
       head = word(PSG_OP_QBEGIN, PSG_Q_EXISTS_VI, slot);
     }
@@ -463,45 +450,6 @@ struct Compiler {
     const int end = emit(word(PSG_OP_QEND));
     code[end_at] = end;
   }
-  // Candidate sources of V.exists(v => body): every term v is compared with
-  void witnesses(int e, std::vector<int>& exprs, std::vector<std::pair<int, int>>& fsets) {
-    const Node& q = T.nodes[e];
-    const int v = q.uid;
-    std::vector<int> w;
-    T.walk(q.a, w);
-    std::set<int> inner;
-    for (int x : w)
-      if (T.nodes[x].k == QUANT || T.nodes[x].k == CONTAINS) inner.insert(T.nodes[x].uid);
-    bool seen = false;
-    for (int x : w) {
-      const Node& b = T.nodes[x];
-      if (b.k != BIN || b.op < PSG_OP_EQ || b.op > PSG_OP_GE) continue;
-      const int pairs[2][2] = {{b.a, b.b}, {b.b, b.a}};
-      for (auto& pr : pairs) {
-        const Node& a = T.nodes[pr[0]];
-        if (a.k != VAR || a.uid != v) continue;
-        std::set<int> bound, fv;
-        T.free_vars(pr[1], bound, fv);
-        if (fv.count(v)) throw SpecError("V.exists variable compared with a term containing itself");
-        const Node& t = T.nodes[pr[1]];
-        if (t.k == FIELD) {
-          const std::pair<int, int> key{t.f, t.tag};
-          bool have = false;
-          for (auto& k : fsets) have = have || k == key;
-          if (!have) fsets.push_back(key);
-        } else {
-          bool dep = false;
-          for (int u : fv) dep = dep || inner.count(u);
-          if (dep) throw SpecError("V.exists witness term depends on an inner bound variable and is not a process field");
-          exprs.push_back(pr[1]);
-        }
-        seen = true;
-      }
-    }
-    for (int x : w)
-      if (T.nodes[x].k == VAR && T.nodes[x].uid == v && !seen)
-        throw SpecError("a V.exists variable may only appear directly in comparisons");
-  }
   int root(int e) {
     const int at = (int)code.size();
     expr(e, 0, false);
@@ -510,33 +458,22 @@ struct Compiler {
   }
 };
 
-bool uses_old(const Tree& T, int e) {
-  std::vector<int> w;
-  T.walk(e, w);
-  for (int x : w)
-    if (T.nodes[x].k == FIELD && T.nodes[x].tag == PSG_TAG_OLD) return true;
-  return false;
-}
+}  // namespace
 
-struct Compiled {
-  std::vector<int32_t> code, entry, flags;
-  int32_t term = -1, nvars = 0;
-  std::vector<std::string> names;
-};
-
-Compiled compile_text(const char* text, int alg) {
+ParsedSpec parse_spec(const char* text) {
   Reader rd{text};
   const Sx s = rd.read();
   rd.skip();
   if (*rd.p) throw SpecError("Formula text: trailing input");
   if (!s.is("Spec")) throw SpecError("Formula text: expected (Spec ...)");
-  Tree T;
+  ParsedSpec P;
+  Tree& T = P.T;
   Lower L{T};
-  int phase = 1;
-  std::vector<int> invs;
+  int& phase = P.phase;
+  std::vector<int>& invs = P.invs;
   std::vector<std::vector<int>> rinv;
-  std::vector<std::pair<std::string, int>> props;
-  int sp = -1;
+  std::vector<std::pair<std::string, int>>& props = P.props;
+  int& sp = P.sp;
   const Lower::Env env;
   for (size_t k = 1; k < s.items.size(); ++k) {
     const Sx& part = s.items[k];
@@ -575,6 +512,13 @@ Compiled compile_text(const char* text, int alg) {
   }
   if (guard >= 0)
     for (int& inv : invs) inv = T.bin(PSG_OP_AND, inv, guard);
+  return P;
+}
+
+Compiled compile_program(ParsedSpec& P, int alg) {
+  Tree& T = P.T;
+  const std::vector<int>& invs = P.invs;
+  const int sp = P.sp;
   Compiler C{T, alg != 0, alg != 0 ? alg_fields(alg) : std::set<int>{}};
   Compiled out;
   if (!invs.empty()) {
@@ -589,7 +533,7 @@ Compiled compile_text(const char* text, int alg) {
       out.flags.push_back(0);
     }
   }
-  for (auto& p : props) {
+  for (auto& p : P.props) {
     if (p.first == "Termination") {
       out.term = C.root(p.second);
       continue;
@@ -617,51 +561,56 @@ void put(char* buf, size_t len, const std::string& s) {
   buf[k] = 0;
 }
 
-}  // namespace
+int fill_program(const Compiled& c, int alg, psg_spec_program* out, char* names, size_t names_len, char* err,
+                 size_t err_len) {
+  std::string joined;
+  for (size_t k = 0; k < c.names.size(); ++k) joined += (k ? "\n" : "") + c.names[k];
+  if (names && names_len <= joined.size()) {  // never a silently truncated slot-name list
+    put(err, err_len, "names buffer too small: " + std::to_string(joined.size() + 1) + " bytes needed");
+    return PSG_ERANGE;
+  }
+  int32_t* code = (int32_t*)std::malloc(sizeof(int32_t) * c.code.size());
+  int32_t* ent = (int32_t*)std::malloc(sizeof(int32_t) * c.entry.size());
+  int32_t* flg = (int32_t*)std::malloc(sizeof(int32_t) * c.flags.size());
+  if (!code || !ent || !flg) {
+    std::free(code);
+    std::free(ent);
+    std::free(flg);
+    put(err, err_len, "out of host memory");
+    return PSG_ENOMEM;
+  }
+  std::memcpy(code, c.code.data(), sizeof(int32_t) * c.code.size());
+  std::memcpy(ent, c.entry.data(), sizeof(int32_t) * c.entry.size());
+  std::memcpy(flg, c.flags.data(), sizeof(int32_t) * c.flags.size());
+  out->n_slots = (int32_t)c.entry.size();
+  out->n_words = (int32_t)c.code.size();
+  out->code = code;
+  out->slot_entry = ent;
+  out->slot_flags = flg;
+  out->term_entry = c.term;
+  out->n_vars = c.nvars;
+  out->module_path = nullptr;
+  out->alg = alg;
+  put(names, names_len, joined);
+  put(err, err_len, "");
+  return PSG_OK;
+}
+
+}  // namespace psgspec
 
 extern "C" {
 
 int psg_spec_from_text(const char* text, int32_t alg, psg_spec_program* out, char* names, size_t names_len,
                        char* err, size_t err_len) {
+  using namespace psgspec;
   if (!text || !out) {
     put(err, err_len, "null argument");
     return PSG_EINVAL;
   }
   std::memset(out, 0, sizeof(*out));
   try {
-    Compiled c = compile_text(text, alg);
-    int32_t* code = (int32_t*)std::malloc(sizeof(int32_t) * c.code.size());
-    int32_t* ent = (int32_t*)std::malloc(sizeof(int32_t) * c.entry.size());
-    int32_t* flg = (int32_t*)std::malloc(sizeof(int32_t) * c.flags.size());
-    if (!code || !ent || !flg) {
-      std::free(code);
-      std::free(ent);
-      std::free(flg);
-      put(err, err_len, "out of host memory");
-      return PSG_ENOMEM;
-    }
-    std::memcpy(code, c.code.data(), sizeof(int32_t) * c.code.size());
-    std::memcpy(ent, c.entry.data(), sizeof(int32_t) * c.entry.size());
-    std::memcpy(flg, c.flags.data(), sizeof(int32_t) * c.flags.size());
-    out->n_slots = (int32_t)c.entry.size();
-    out->n_words = (int32_t)c.code.size();
-    out->code = code;
-    out->slot_entry = ent;
-    out->slot_flags = flg;
-    out->term_entry = c.term;
-    out->n_vars = c.nvars;
-    out->module_path = nullptr;
-    out->alg = alg;
-    std::string joined;
-    for (size_t k = 0; k < c.names.size(); ++k) joined += (k ? "\n" : "") + c.names[k];
-    if (names && names_len <= joined.size()) {  // never a silently truncated slot-name list
-      psg_spec_release(out);
-      put(err, err_len, "names buffer too small: " + std::to_string(joined.size() + 1) + " bytes needed");
-      return PSG_ERANGE;
-    }
-    put(names, names_len, joined);
-    put(err, err_len, "");
-    return PSG_OK;
+    ParsedSpec P = parse_spec(text);
+    return fill_program(compile_program(P, alg), alg, out, names, names_len, err, err_len);
   } catch (const std::exception& e) {
     put(err, err_len, e.what());
     return PSG_EINVAL;

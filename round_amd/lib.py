@@ -25,6 +25,7 @@ EXPORTED_SYMBOLS = [
     "psg_selftest_map_head", "psg_load_inputs_f64", "psg_copy_decisions_f64", "psg_fetch_instances_f64",
     "psg_run_batch_spec", "psg_load_schedule", "psg_clear_schedule", "psg_materialize_schedule",
     "psg_population_fresh", "psg_population_next", "psg_population_read", "psg_spec_from_text", "psg_spec_release",
+    "psg_spec_compile_native", "psg_spec_native_source",
 ]
 
 
@@ -78,6 +79,10 @@ def load():
     L.psg_population_read.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
     L.psg_spec_from_text.argtypes = [C.c_char_p, C.c_int32, C.POINTER(abi.SpecProgram), C.c_char_p, C.c_size_t,
                                      C.c_char_p, C.c_size_t]
+    L.psg_spec_compile_native.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
+                                          C.POINTER(abi.SpecProgram), C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
+    L.psg_spec_native_source.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
+                                         C.POINTER(C.c_size_t), C.c_char_p, C.c_size_t]
     L.psg_spec_release.argtypes = [C.POINTER(abi.SpecProgram)]
     L.psg_spec_release.restype = None
     L.psg_selftest_map_head.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
@@ -343,3 +348,49 @@ def spec_from_text(text, alg=0):
         return prog
     finally:
         L.psg_spec_release(C.byref(cp))
+
+
+def spec_compile_native(text, alg=0, fused=False, n=0, cache_dir=None):
+    """psg_spec_compile_native (host code, hiprtc, no GPU needed): Formula text -> a
+    formula.Program whose module_path is the natively lowered (fused: with the round kernel)
+    code object, compiled in-process by the library."""
+    from . import formula
+    L = load()
+    cp = abi.SpecProgram()
+    err = C.create_string_buffer(8192)
+    names = C.create_string_buffer(1 << 16)
+    rc = L.psg_spec_compile_native(text.encode(), int(alg), 1 if fused else 0, int(n),
+                                   cache_dir.encode() if cache_dir else None, C.byref(cp), names, len(names),
+                                   err, len(err))
+    if rc != 0:
+        raise formula.FormulaError(err.value.decode() or f"psg_spec_compile_native rc={rc}")
+    try:
+        code = [cp.code[k] for k in range(cp.n_words)]
+        entry = [cp.slot_entry[k] for k in range(cp.n_slots)]
+        flags = [cp.slot_flags[k] for k in range(cp.n_slots)]
+        prog = formula.Program(code, entry, flags, cp.term_entry, cp.n_vars, names.value.decode().split("\n"), None)
+        prog.alg = cp.alg
+        prog.module_path = cp.module_path.decode()
+        return prog
+    finally:
+        path = cp.module_path
+        L.psg_spec_release(C.byref(cp))
+        del path
+
+
+def spec_native_source(text, alg=0, fused=False, n=0):
+    """psg_spec_native_source: the HIP source psg_spec_compile_native compiles (no compile)."""
+    from . import formula
+    L = load()
+    err = C.create_string_buffer(8192)
+    size = C.c_size_t(0)
+    rc = L.psg_spec_native_source(text.encode(), int(alg), 1 if fused else 0, int(n), None, C.byref(size), err,
+                                  len(err))
+    if rc not in (0, abi.PSG_ERANGE):
+        raise formula.FormulaError(err.value.decode() or f"psg_spec_native_source rc={rc}")
+    buf = C.create_string_buffer(size.value)
+    rc = L.psg_spec_native_source(text.encode(), int(alg), 1 if fused else 0, int(n), buf, C.byref(size), err,
+                                  len(err))
+    if rc != 0:
+        raise formula.FormulaError(err.value.decode() or f"psg_spec_native_source rc={rc}")
+    return buf.value.decode()

@@ -33,6 +33,11 @@ def jobs():
     out.append(("lv_custom", abi.PSG_ALG_LAST_VOTING, False, None))
     out.append(("ref", abi.PSG_ALG_OTR, True, 64))
     out.append(("ref", abi.PSG_ALG_LAST_VOTING, True, 64))
+    # the Formula-text route (psg_spec_compile_native: the library's own generator + hiprtc),
+    # tests/test_spec_native_text.py, tests/test_jni_shim.py and the G1 *_text rows
+    for a, n in ((abi.PSG_ALG_OTR, 64), (abi.PSG_ALG_LAST_VOTING, 64), (abi.PSG_ALG_OTR2, 100),
+                 (abi.PSG_ALG_BENOR, 128)):
+        out.append(("text", a, True, n))
     return sorted(set(out), key=str)
 
 
@@ -40,6 +45,9 @@ def build(job):
     from round_amd import formula as F
     import spec_cases
     kind, alg, fused, n = job
+    if kind == "text":  # compiled in-process by libpsg (hiprtc), as the JVM plugin would
+        from round_amd import lib
+        return os.path.basename(lib.spec_compile_native(F.to_text(F.REFERENCE_SPECS[alg]()), alg, fused, n).module_path)
     if kind in ("ref", "fusedbuild"):
         spec = F.REFERENCE_SPECS[alg]() if alg in F.REFERENCE_SPECS else spec_cases.uniform_agreement()
     elif kind == "lv_custom":

@@ -244,3 +244,31 @@ def test_batch_through_the_shim_equals_the_python_binding(shim):
         assert shim.values(FJ_INT, fr) == [v for x in rec2 for v in (x.decision, x.decision_round, x.halt_round,
                                                                          x.final_x)]
         assert ssum[:-1] == abi.summary_to_list(sp.summary)[:-1]
+
+
+@pytest.mark.gpu
+def test_native_spec_through_the_shim(shim):
+    """compileSpecNative (psg_spec_compile_native) + runBatchSpec with its module: the fused
+    text-lowered OTR Spec gives the built-in checker's counters (the JVM's fast route)."""
+    n, R, count, V = 64, 20, 4000, 64
+    create = shim.fn("create", C.c_int64, *([C.c_int32] * 3 + [C.c_int64] + [C.c_int32] * 3 + [C.c_double] +
+                                            [C.c_int32] * 3 + [C.c_int64] + [C.c_int32] * 5 + [C.c_uint8, C.c_void_p]))
+    h = create(abi.PSG_ALG_OTR, n, R, 2, V, 2, 0, 0.0, 0, 0, 0, count, 3, 1 << 30, -1, -1, -1, 1, None)
+    assert h != 0, shim.exception()
+    text = shim.L.fj_string(F.to_text(F.otr_spec()).encode())
+    packed = shim.values(FJ_INT, shim.fn("compileSpec", C.c_void_p, C.c_void_p, C.c_int32)(text, abi.PSG_ALG_OTR))
+    path = shim.fn("compileSpecNative", C.c_void_p, C.c_void_p, C.c_int32, C.c_uint8, C.c_int32)(
+        text, abi.PSG_ALG_OTR, 1, n)
+    assert path and shim.exception() is None
+    ns, nw = packed[0], packed[1]
+    rbs = shim.fn("runBatchSpec", C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                  C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p)
+    ssum = shim.values(FJ_LONG, rbs(h, 0, count, shim.array(FJ_INT, packed[4:4 + nw]),
+                                    shim.array(FJ_INT, packed[4 + nw:4 + nw + ns]),
+                                    shim.array(FJ_INT, packed[4 + nw + ns:]), packed[2], packed[3],
+                                    abi.PSG_ALG_OTR, path, None))
+    summ = shim.values(FJ_LONG, shim.fn("runBatch", C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p)(
+        h, 0, count, None))
+    shim.fn("destroy", None, C.c_int64)(h)
+    assert shim.exception() is None and shim.L.fj_take_oob() == 0
+    assert ssum[:-1] == summ[:-1]

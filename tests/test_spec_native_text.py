@@ -1,0 +1,93 @@
+"""Native Spec lowering from Formula text through the C ABI (psg_spec_compile_native).
+
+The JVM plugin hands a psync.Spec to the library as Formula text (integration/scala/
+GpuSpec.scala). psg_spec_from_text compiles it to bytecode; psg_spec_compile_native also
+lowers it to native gfx950 code in-process — the generator of round_amd/formula.py
+(codegen_hip, _fused_source) restated in C++ (round_amd/csrc/psg_spec_gen.cpp), compiled
+with hiprtc, cached under formula.compile_native's key. CPU tests: the C++ source is byte
+for byte the one Python generates from the same text (formula.from_text), for the reference
+Specs, every custom Spec of the GPU suites and FormulaExtractor-shaped texts, native and
+fused; a hiprtc compile yields a gfx950 code object whose program equals psg_spec_from_text's.
+GPU tests: the library-compiled fused module's results equal the built-in checker's and the
+Python-compiled module's, word for word.
+"""
+import os
+
+import pytest
+
+from round_amd import abi, formula as F, lib, psync
+
+import spec_cases
+import test_spec_text as TT
+
+
+def _python_source(text, alg, fused, n):
+    src, _ = F.codegen_hip(F.from_text(text), alg)
+    if fused:
+        src = "#define PSG_FUSED_MODULE 1\n" + src + F._fused_source(alg, [(n + 63) // 64])
+    return src
+
+
+CASES = [(f"ref-{a}", a, 64, lambda a=a: F.to_text(F.REFERENCE_SPECS[a]())) for a in sorted(F.REFERENCE_SPECS)]
+CASES += [(c[0], c[1].alg_id, c[2], lambda mk=c[4]: F.to_text(mk())) for c in spec_cases.CUSTOM]
+CASES += [("let", abi.PSG_ALG_LAST_VOTING, 8, lambda: TT.LV_MAJORITY_LET),
+          ("flat-binders", abi.PSG_ALG_OTR, 8, lambda: TT.AGREEMENT_FLAT),
+          ("nary-and", abi.PSG_ALG_BENOR, 8, lambda: TT.NARY_AND)]
+
+
+@pytest.mark.parametrize("cid,alg,n,text", CASES, ids=[c[0] for c in CASES])
+def test_native_source_equals_python(cid, alg, n, text):
+    t = text()
+    for fused in (False, True):
+        if fused and alg not in F.FUSED_KERNELS:
+            continue
+        assert lib.spec_native_source(t, alg, fused, n) == _python_source(t, alg, fused, n), (cid, fused)
+
+
+def test_native_source_rejects_like_the_bytecode_compiler():
+    with pytest.raises(F.FormulaError, match="ForAll over Int"):
+        lib.spec_native_source("(Spec (invariants (ForAll ((v Int)) (App Gt (Var v) (Lit 0)))))", abi.PSG_ALG_OTR)
+    with pytest.raises(F.FormulaError, match="no integer state"):
+        lib.spec_native_source(F.to_text(F.otr_spec()), abi.PSG_ALG_EPSILON, True, 64)
+
+
+def test_hiprtc_compile_on_the_host(tmp_path):
+    """In-process compile (no GPU): a gfx950 code object in the given cache, the program of
+    psg_spec_from_text, the cached object reused by a second call."""
+    text = F.to_text(F.otr_spec())
+    prog = lib.spec_compile_native(text, abi.PSG_ALG_OTR, True, 64, cache_dir=str(tmp_path))
+    assert prog.module_path.startswith(str(tmp_path)) and os.path.getsize(prog.module_path) > 10_000
+    with open(prog.module_path, "rb") as f:
+        assert f.read(4) == b"\x7fELF"
+    TT._same(prog, lib.spec_from_text(text, abi.PSG_ALG_OTR))
+    mtime = os.path.getmtime(prog.module_path)
+    again = lib.spec_compile_native(text, abi.PSG_ALG_OTR, True, 64, cache_dir=str(tmp_path))
+    assert again.module_path == prog.module_path and os.path.getmtime(again.module_path) == mtime
+    # the cache key is formula.compile_native's: the Python route finds this very file
+    assert F.compile_native(F.from_text(text), abi.PSG_ALG_OTR, fused=True, n=64,
+                            cache_dir=str(tmp_path)).module_path == prog.module_path
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg,mk,n,count,kw", [
+    (psync.OTR(), F.otr_spec, 64, 20_000, dict(value_range=64, seed=2)),
+    (psync.LastVoting(), F.lv_spec, 64, 5_000, dict(seed=7)),
+    (psync.OTR2(), F.otr2_spec, 100, 2_000, dict(value_range=4, seed=3)),
+    (psync.BenOr(), F.benor_spec, 128, 2_000, dict(seed=5)),
+], ids=["otr", "lv", "otr2-n100", "benor-n128"])
+def test_text_fused_module_equals_builtin_and_python(alg, mk, n, count, kw):
+    """The Spec given as text, lowered and compiled by the library (hiprtc; built into the
+    default cache by __graft_entry__.build(), scripts/precompile_specs.py), run fused: every
+    counter and per-instance result equals the built-in checker's and the Python-compiled
+    module's (hipcc, from the DSL Spec), word for word."""
+    text = F.to_text(mk())
+    prog_c = lib.spec_compile_native(text, alg.alg_id, True, n)
+    prog_py = F.compile_native(mk(), alg.alg_id, fused=True, n=n)
+    with psync.GpuRound(alg, n, batch_capacity=count, **kw) as g:
+        builtin = g.run(0, count, per_instance=True)
+        rc = g.run_spec(0, count, prog_c, per_instance=True)
+        rp = g.run_spec(0, count, prog_py, per_instance=True)
+    key = lambda r: (abi.summary_to_list(r.summary)[:-1],
+                     [(s.digest, tuple(s.first_fail), s.term_round) for s in r.per_instance])
+    assert key(rc) == key(rp)
+    assert key(rc) == key(builtin)
