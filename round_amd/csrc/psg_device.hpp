@@ -1002,9 +1002,9 @@ struct CrashSets {
   }
   PSG_DEV void sets(Grp<W>& g, int k, Mask<W>& CB, Mask<W>& CN) const {
     // crashed before round k: 0 <= cr < k, one unsigned compare (cr = -1: correct)
-    if constexpr (W == 1) {
-      CB = g.ballot((uint32_t)cr[0] < (uint32_t)k);
-      CN = g.ballot(cr[0] == k);
+    if constexpr (W == 1) {  // (lanes past n have crash round -1: no valid-lane mask needed)
+      CB = g.ballot_any((uint32_t)cr[0] < (uint32_t)k);
+      CN = g.ballot_any(cr[0] == k);
     } else {
 #pragma unroll
       for (int w = 0; w < W; ++w) {
@@ -1069,11 +1069,28 @@ PSG_DEV void counters_flush(BlockCounters* bc, unsigned long long* g, int ncheck
   }
 }
 
+// Per-lane running sum of the process-round steps over a wave's instances (C_ACTIVE), reduced
+// and flushed once per wave instead of a wave reduction per instance.
+struct StepTally {
+  uint64_t steps = 0;  // this lane's processes' steps over the wave's instances
+  PSG_DEV void add(int32_t s) { steps += (uint64_t)(uint32_t)s; }
+  // every lane of the wave, converged; one LDS atomic per wave
+  PSG_DEV void flush(BlockCounters* bc) {
+    Grp<1> g1;
+    const uint64_t t = g1.wave_sum64(steps);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&bc->active, (unsigned long long)t);
+  }
+};
+
 // Per-instance epilogue: digest, decide results, summaries, counters.
 // Called by every lane of the group; lane values are this process's results.
+// tally (optional): accumulate the steps per lane (StepTally::flush at the end of the kernel)
+// instead of a wave sum per instance; live_rounds >= 0: the rounds the instance executed (some
+// process active), known to the caller, instead of a wave maximum.
 template <int W>
 PSG_DEV void finish_instance(Grp<W>& g, const KArgs& a, uint64_t i, const Checks& ck, int nchecks, int32_t dec_val,
-                             int32_t dec_round, int32_t halt_round, int32_t main_x, BlockCounters* bc) {
+                             int32_t dec_round, int32_t halt_round, int32_t main_x, BlockCounters* bc,
+                             StepTally* tally = nullptr, int32_t live_rounds = -1) {
   const int n = a.n;
   const bool decided = dec_round >= 0;
   const uint64_t d = g.valid ? proc_digest(g.pid, dec_val, dec_round, halt_round, main_x) : 0ull;
@@ -1081,8 +1098,10 @@ PSG_DEV void finish_instance(Grp<W>& g, const KArgs& a, uint64_t i, const Checks
   const int nd = mpopc(g.ballot(decided));
   // rounds in which this process took a step: up to and including its halting round
   const int32_t steps = g.valid ? (halt_round >= 0 ? halt_round + 1 : a.R) : 0;
-  const uint32_t wave_steps = Grp<W>::wave_sum32((uint32_t)steps);
-  const int32_t live = g.max32(steps, true);  // rounds executed for the instance
+  uint32_t wave_steps = 0;
+  if (tally) tally->add(steps);
+  else wave_steps = Grp<W>::wave_sum32((uint32_t)steps);
+  const int32_t live = live_rounds >= 0 ? live_rounds : g.max32(steps, true);  // rounds executed for the instance
   if (g.valid) {
     const uint64_t off = i * (uint64_t)n + (uint64_t)g.pid;
     if (a.out_decision) a.out_decision[off] = dec_val;
@@ -1116,7 +1135,7 @@ PSG_DEV void finish_instance(Grp<W>& g, const KArgs& a, uint64_t i, const Checks
       atomicAdd(&bc->live, (unsigned long long)live);
     }
   }
-  if (g.lane == 0) atomicAdd(&bc->active, (unsigned long long)wave_steps);
+  if (!tally && g.lane == 0) atomicAdd(&bc->active, (unsigned long long)wave_steps);
 }
 
 // Process state at check point c for the Spec-program interpreter

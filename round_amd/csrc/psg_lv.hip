@@ -64,7 +64,7 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, int32_t r4, int
   // binary search's bookkeeping runs in uniform VGPRs; the formulas are those of the
   // reference form below (kept for A/B: -DPSG_LV_CHECK_V2=0).
   const uint32_t dec01 = fl & F_DECIDED;  // F_DECIDED == 1
-  const Mask<W> D = g.ballot(dec01 != 0u);
+  const Mask<W> D = g.ballot_any(dec01 != 0u);  // never set past n
   const bool anyD = many(D);
   const int32_t d0 = anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
   if (PSG_LV_EXP == 2) { ck.record(0, meq(D, full), c, g.lane); return; }
@@ -302,7 +302,7 @@ PSG_DEV void lv_body(const KArgs& a) {
       constexpr int RS = decltype(RSc)::value;
       const uint32_t old_fl = fl;
       const int32_t old_decision = decision;
-      const Mask<W> act = g.ballot((fl & F_HALTED) == 0u);
+      const Mask<W> act = g.ballot_any((fl & F_HALTED) == 0u);  // lanes past n are halted
       int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
         const int c = cph;
@@ -317,7 +317,7 @@ PSG_DEV void lv_body(const KArgs& a) {
         constexpr bool coordRound = (RS & 1) == 0;
         // R1 / R3: does the coordinator send (commit / ready, LastVoting.scala:141, 187)? When it
         // does not, no mailbox is read and no HO bit of the round is observed
-        const bool sent = !coordRound && cAlive && mtest(g.ballot((fl & (RS == 1 ? F_COMMIT : F_READY)) != 0u), c);
+        const bool sent = !coordRound && cAlive && mtest(g.ballot_any((fl & (RS == 1 ? F_COMMIT : F_READY)) != 0u), c);
         Mask<W> HO = mzero<W>(), HOc = mzero<W>();
         if constexpr (XHO) {
           HO = sc.ho(k, g.pid, good, goodS, CB, CN);
@@ -358,7 +358,7 @@ PSG_DEV void lv_body(const KArgs& a) {
             ts = rcv ? phase : ts;
           }
         } else if constexpr (RS == 2) {  // R2: ts == r/4 send x to coord; coord ready on a majority
-          const Mask<W> Mc = mand(mand(HOc, act), g.ballot(ts == phase));
+          const Mask<W> Mc = mand(mand(HOc, act), g.ballot_any(ts == phase));  // ts = -1 past n
           hs = g.pid == c ? mpopc(Mc) : 0;
           if (cAlive && mpopc(Mc) > need2 && g.pid == c) fl |= F_READY;
         } else {  // R3: coord broadcasts vote if ready; receivers decide and exit

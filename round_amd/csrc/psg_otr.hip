@@ -38,16 +38,17 @@ struct OtrLds {
 // V.exists(v => |{i : i.x == v}| > 2n/3 && all decisions == v): with decisions only
 // v = d0 can qualify; without, v must be a strict majority (Boyer-Moore candidate).
 template <int W, bool V2>
+// od / ox: "decision / x maybe not initial" (X0Set::maybe_out01_2 of the current values), probed
+// by the caller when the values change (round 0 and executed updates) instead of at every check
+// point: the memoized probe of the fused lowering; every formula is still evaluated.
 PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, int c, bool has_old, int n,
                        const Mask<W>& full, int32_t x, uint32_t dec01, int32_t decision, uint32_t old01,
-                       int32_t old_decision, uint32_t valid01) {
+                       int32_t old_decision, uint32_t valid01, uint32_t od, uint32_t ox) {
   const int sthr = (2 * n) / 3;  // 2*n/3 in the Spec (Otr.scala:101)
   if constexpr (W > 1) {
     L.ds[g.pid] = decision;
     __syncthreads();
   }
-  uint32_t od, ox;
-  X0.maybe_out01_2(decision, x, od, ox);
   const uint32_t irr01 = has_old ? old01 & (1u - (dec01 & eq01(old_decision, decision))) : 0u;
   {
     // Settled state first (every process decided, every decision equal to process 0's, no
@@ -127,6 +128,7 @@ PSG_DEV void otr_body(const KArgs& a) {
   PhaseTimers pt;  // profiling builds only: t0 setup, t1 active round, t2 frozen round, t3 finish
   pt.start();
   InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
+  StepTally tally;     // per-lane process-round steps, reduced once per wave
   // Host-supplied initial values are loaded one instance ahead: the next row's load is
   // issued when an instance starts and consumed when the next one does, so its latency
   // overlaps the current instance's rounds instead of stalling its setup.
@@ -154,12 +156,14 @@ PSG_DEV void otr_body(const KArgs& a) {
     X0.build(g, x0tab[grp], x0);
     // OtrProcess state after init(io) (Otr.scala:15-26); flags are 0/1 lane words
     int32_t x = x0, decision = -1, after = a.param;
+    uint32_t od, ox;  // memoized X0 probes of decision / x (otr_check)
+    X0.maybe_out01_2(decision, x, od, ox);
     uint32_t dec01 = 0, halted01 = 1u - valid01;
     int32_t dec_val = 0, dec_round = -1, halt_round = -1;
     Checks ck;
     ck.reset();
     typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
-    if constexpr (!SH::kFused) otr_check<W, V2>(g, L, X0, ck, 0, false, n, full, x, dec01, decision, 0u, -1, valid01);
+    if constexpr (!SH::kFused) otr_check<W, V2>(g, L, X0, ck, 0, false, n, full, x, dec01, decision, 0u, -1, valid01, od, ox);
     // OTR2's decision is an Option (PSG_NONE32 when empty)
     auto trace = [&](int c, int32_t hs) {
       emit_state<W, SH>(sh, g, a, i, c, x, (int32_t)dec01, V2 && !dec01 ? PSG_NONE32 : decision, 0, 0, 0, 0, 0, hs);
@@ -167,12 +171,14 @@ PSG_DEV void otr_body(const KArgs& a) {
     if (tracing_on) trace(0, n);
     pt.mark(0);
 
+    int32_t live_rounds = 0;  // rounds in which some process took a step
     for (int k = 0; k < a.R; ++k) {
       const uint32_t old01 = dec01;
       const int32_t old_decision = decision;
       const Mask<W> act = g.ballot_any(halted01 == 0u);  // lanes past n are halted
       int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
       if (many(act)) {
+        live_rounds = k + 1;
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
@@ -241,6 +247,7 @@ PSG_DEV void otr_body(const KArgs& a) {
           dec_round = first ? k : dec_round;
           decision = newdec ? best_v : decision;
           dec01 |= newdec;
+          if constexpr (!SH::kFused) X0.maybe_out01_2(decision, x, od, ox);
         }
         // after -= 1 once decided; exitAtEndOfRound when it reaches 0 (Otr.scala:75-80)
         const uint32_t ad = (1u - halted01) & dec01;
@@ -249,14 +256,17 @@ PSG_DEV void otr_body(const KArgs& a) {
         halt_round = h ? k : halt_round;
         halted01 |= h;
       }
-      if constexpr (!SH::kFused) otr_check<W, V2>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, old01, old_decision, valid01);
+      if constexpr (!SH::kFused)
+        otr_check<W, V2>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, old01, old_decision, valid01, od, ox);
       if (tracing_on) trace(k + 1, hs);
       pt.mark(many(act) ? 1 : 2);
     }
-    finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 8, dec_val, dec_round, halt_round, x, &bc);
+    finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 8, dec_val, dec_round, halt_round, x, &bc,
+                       &tally, live_rounds);
     pt.mark(3);
   }
   pt.flush(a.counters, threadIdx.x & 63);
+  tally.flush(&bc);
   __syncthreads();
   counters_flush(&bc, a.counters, SH::kFused ? SH::kSlots : 8, a.R);
 }

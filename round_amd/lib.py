@@ -79,10 +79,14 @@ def load():
     L.psg_population_read.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
     L.psg_spec_from_text.argtypes = [C.c_char_p, C.c_int32, C.POINTER(abi.SpecProgram), C.c_char_p, C.c_size_t,
                                      C.c_char_p, C.c_size_t]
-    L.psg_spec_compile_native.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
-                                          C.POINTER(abi.SpecProgram), C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
-    L.psg_spec_native_source.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
-                                         C.POINTER(C.c_size_t), C.c_char_p, C.c_size_t]
+    try:  # (A/B builds of older kernels, PSG_LIB, may predate these; test_abi checks the in-tree library)
+        L.psg_spec_compile_native.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
+                                              C.POINTER(abi.SpecProgram), C.c_char_p, C.c_size_t, C.c_char_p,
+                                              C.c_size_t]
+        L.psg_spec_native_source.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
+                                             C.POINTER(C.c_size_t), C.c_char_p, C.c_size_t]
+    except AttributeError:
+        pass
     L.psg_spec_release.argtypes = [C.POINTER(abi.SpecProgram)]
     L.psg_spec_release.restype = None
     L.psg_selftest_map_head.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
