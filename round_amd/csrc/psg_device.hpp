@@ -393,11 +393,13 @@ PSG_DEV bool meq(const Mask<W>& a, const Mask<W>& b) {
 }
 template <int W>
 PSG_DEV bool mtest(const Mask<W>& a, int q) {
-  uint64_t word = a.w[0];
+  // an AND with a per-word bit (not a word select: LLVM turns a select chain over a
+  // uniform index back into a private-array load, i.e. a scratch round trip)
+  const uint64_t bit = 1ull << (q & 63);
+  uint64_t hit = 0;
 #pragma unroll
-  for (int i = 1; i < W; ++i)
-    if ((q >> 6) == i) word = a.w[i];
-  return (word >> (q & 63)) & 1ull;
+  for (int i = 0; i < W; ++i) hit |= a.w[i] & (((q >> 6) == i) ? bit : 0ull);
+  return hit != 0;
 }
 template <int W>
 PSG_DEV void mset(Mask<W>& a, int q) {
@@ -1425,7 +1427,7 @@ PSG_DEV int32_t majority_candidate(Grp<W>& g, int32_t x) {
 // needed when the maximal-ts senders disagree on x.
 template <int W>
 PSG_DEV int32_t maxby_ts_x(Grp<W>& g, const int32_t* xs, const Mask<W>& Mc, int size, int32_t x, int32_t ts,
-                           uint32_t myh, int tiebreak) {
+                           uint32_t myh, int tiebreak, const ChampTable<W>* CT = nullptr) {
   const bool inMc = mtest(Mc, g.pid);
   const int32_t maxts = g.max32(ts, inMc);
   const Mask<W> T = mand(Mc, g.ballot(ts == maxts));
@@ -1436,13 +1438,28 @@ PSG_DEV int32_t maxby_ts_x(Grp<W>& g, const int32_t* xs, const Mask<W>& Mc, int 
   if (differ && tiebreak == PSG_TIE_CHAMP && size > 4) {
     // payload depth of each candidate = longest 5-bit hash prefix shared with another entry
     int depth = 0;
+    if (CT) {
+      // per lane, level by level: the entries sharing this lane's first l+1 fragments are the
+      // mailbox intersected with the table's fragment masks; depth = the levels where that set
+      // still holds another entry (lane-parallel VALU + LDS instead of a scalar walk of the
+      // mailbox with a hash per entry)
+      Mask<W> S = Mc;
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      uint64_t m = Mc.w[w];
-      while (m) {
-        const int f = w * 64 + __builtin_ctzll(m);
-        m &= m - 1;
-        if (f != g.pid) depth = max(depth, champ_cpl(myh, scala_improve((uint32_t)f)));
+      for (int l = 0; l < 7; ++l) {
+        const uint32_t f = (myh >> (5 * l)) & 31u;
+#pragma unroll
+        for (int w = 0; w < W; ++w) S.w[w] &= CT->b[l][f][w];
+        depth += mpopc(S) >= 2 ? 1 : 0;
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        uint64_t m = Mc.w[w];
+        while (m) {
+          const int f = w * 64 + __builtin_ctzll(m);
+          m &= m - 1;
+          if (f != g.pid) depth = max(depth, champ_cpl(myh, scala_improve((uint32_t)f)));
+        }
       }
     }
     const bool inT = mtest(T, g.pid);

@@ -250,7 +250,9 @@ PSG_DEV void lv_body(const KArgs& a) {
   __shared__ int64_t red[2 * W];
   __shared__ LvLds<W> L;
   __shared__ int32_t x0tab[Geometry<W>::kGroups][X0Set<W>::kSlots];
+  __shared__ ChampTable<W> CT;  // CHAMP fragment masks per level (maxBy's first max in Map order)
   counters_init(&bc);
+  if (a.tiebreak == PSG_TIE_CHAMP) CT.build(a.n);
   __syncthreads();
   Grp<W> g;
   grp_setup(g, a, xb, red);
@@ -341,7 +343,7 @@ PSG_DEV void lv_body(const KArgs& a) {
           const int size = mpopc(Mc);
           hs = g.pid == c ? size : 0;
           if (cAlive && (size > n / 2 || (k == 0 && size > 0))) {
-            const int32_t v = maxby_ts_x<W>(g, L.xs, Mc, size, x, ts, myh, a.tiebreak);
+            const int32_t v = maxby_ts_x<W>(g, L.xs, Mc, size, x, ts, myh, a.tiebreak, &CT);
             if (g.pid == c) {
               vote = v;
               fl |= F_COMMIT;

@@ -139,7 +139,7 @@ PSG_DEV void slv_body(const KArgs& a) {
           const int size = mpopc(Mc);
           hs = g.pid == c ? size : 0;
           if (cAlive && size > n / 2) {
-            const int32_t v = maxby_ts_x<W>(g, L.xs, Mc, size, x, ts, myh, a.tiebreak);
+            const int32_t v = maxby_ts_x<W>(g, L.xs, Mc, size, x, ts, myh, a.tiebreak, &CT);
             if (g.pid == c) {
               vote = v;
               fl |= S_COMMIT;
