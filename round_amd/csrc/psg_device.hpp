@@ -395,6 +395,7 @@ template <int W>
 PSG_DEV bool mtest(const Mask<W>& a, int q) {
   // an AND with a per-word bit (not a word select: LLVM turns a select chain over a
   // uniform index back into a private-array load, i.e. a scratch round trip)
+  if (W == 1) return (a.w[0] >> (q & 63)) & 1ull;
   const uint64_t bit = 1ull << (q & 63);
   uint64_t hit = 0;
 #pragma unroll

@@ -54,19 +54,31 @@ PSG_DEV Mask<W> load_t(const uint64_t* ts, int q) {
 // `content.find(_._1)` of receiver p (KSetAgreement.scala:53): the first decider message in
 // Scala Map iteration order — the first pid of cand up to 4 mailbox entries (Map1..Map4)
 // or when the candidates agree on t; otherwise the CHAMP order's first (min sort key).
+// hol / ncols (optional): the round's holder columns (kset_packed): the candidates' t agree
+// iff every column holds all of them or none, so no candidate's t is read.
 template <int W, int CS = 0>
-PSG_DEV int kset_find(const KArgs& a, const uint64_t* ts, const Mask<W>& M, const Mask<W>& cand) {
+PSG_DEV int kset_find(const KArgs& a, const uint64_t* ts, const Mask<W>& M, const Mask<W>& cand,
+                      const uint64_t (*hol)[W] = nullptr, int ncols = 0) {
   int qs = mfirst(cand);
   if (a.tiebreak == PSG_TIE_CHAMP && mpopc(M) > 4 && mpopc(cand) > 1) {
-    const Mask<W> t0 = load_t<W, CS>(ts, qs);
     bool differ = false;
+    if (hol) {
+      for (int c = 0; c < ncols; ++c) {
+        Mask<W> x;
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      uint64_t m = cand.w[w];
-      while (m) {
-        const int q = w * 64 + __builtin_ctzll(m);
-        m &= m - 1;
-        if (!meq(load_t<W, CS>(ts, q), t0)) differ = true;
+        for (int w = 0; w < W; ++w) x.w[w] = cand.w[w] & hol[c][w];
+        differ = differ || (many(x) && !meq(x, cand));
+      }
+    } else {
+      const Mask<W> t0 = load_t<W, CS>(ts, qs);
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        uint64_t m = cand.w[w];
+        while (m) {
+          const int q = w * 64 + __builtin_ctzll(m);
+          m &= m - 1;
+          if (!meq(load_t<W, CS>(ts, q), t0)) differ = true;
+        }
       }
     }
     if (differ) {
@@ -109,13 +121,29 @@ PSG_DEV int kset_find(const KArgs& a, const uint64_t* ts, const Mask<W>& M, cons
 // k-agreement check's ballots are wave ballots; no round needs a block barrier.
 template <int W>
 struct KsPk {
+  static constexpr int kClasses = 8;
   uint64_t ts[64 * W * W];
   int32_t x0s[64 * W];
+  static constexpr int kCols = 32;
+  uint64_t ct[kClasses][W];  // a round's classes of equal t among the alive senders: their t
+  uint64_t ce[kClasses][W];  // ... and their members
+  uint64_t hol[kCols][W];    // holders H_o of each varying origin o (column form, below)
 };
+
+// Wave AND / OR of a per-lane mask (DPP OR reductions; AND = NOT OR NOT).
+template <int W>
+PSG_DEV void pk_and_or(const Mask<W>& a, const Mask<W>& o, Mask<W>& all, Mask<W>& any) {
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const uint64_t na = ~a.w[w];
+    all.w[w] = ~((uint64_t)wave_or((uint32_t)na) | ((uint64_t)wave_or((uint32_t)(na >> 32)) << 32));
+    any.w[w] = (uint64_t)wave_or((uint32_t)o.w[w]) | ((uint64_t)wave_or((uint32_t)(o.w[w] >> 32)) << 32);
+  }
+}
 
 template <int W>
 PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, KsPk<W>& L, int32_t* x0lds,
-                         BlockCounters* bc) {
+                         BlockCounters* bc, PhaseTimers& pt) {
   const int n = a.n, kk = a.param;
   const int need = a.variant == 1 ? 1 : n - kk;  // same.size > n - k (KSetAgreement.scala:56)
   Sched<W, false> sc;
@@ -152,6 +180,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
   ck.reset();
   auto check = [&](int c) { pk_kagree_check<W>(P, ck, c, kk, decided, decision, cr, X0); };
   check(0);
+  pt.mark(0);
   Mask<W> act;
   {
     uint32_t al[W];
@@ -160,7 +189,12 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
     act = P.ballot(al);
   }
   for (int k = 0; k < a.R; ++k) {
-    if (many(act)) {
+    // Every process halted: the state is frozen from here on, and the k-agreement predicate
+    // reads only (decided, decision, crashed, X0) — no round counter — so check points
+    // k+1 .. R evaluate to check point k's result, already recorded (first-failure and
+    // termination are running minima): they are resolved without re-evaluation.
+    if (!many(act)) break;
+    {
       Mask<W> goodS;
       const bool good = sc.good_round(k, P.lane, a.R, goodS);
       Mask<W> CB = mzero<W>(), CN = mzero<W>();
@@ -186,57 +220,144 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
         notown[j] = meq(t[j], own) ? 0u : 1u;
       }
       const bool closed = !many(mand(act, P.ballot(notown)));
-      // one slot at a time (its HO set M, its merge or adoption); the t registers keep the
-      // pre-round state until every slot is done (the class ballots read every slot's t)
-      Mask<W> tnew[W];
-      uint32_t becomeDec[W];
+      // The classes of equal t among the alive senders (same = mailbox.filter(_._2._2 == t).size,
+      // uni = t ++ every received t) are the same for every receiver: found once per round (at
+      // most kClasses; the rest, rem, is walked sender by sender), their t and member masks kept
+      // in this wave's LDS, each slot's class index in cls (4 bits per slot, 15 = none). So the
+      // receivers need only the pre-round staging, not their own pre-round t, and each slot's t
+      // is updated in place (no second set of W x W mask words per lane).
+      //
+      // Column form (the common case, few origins vary): I = the origins every alive sender
+      // holds, U = those some alive sender holds, D = U \ I the varying ones. Every alive t is
+      // I + (t & D), so for a receiver p (alive, M its senders, all alive)
+      //   uni  = t_p + {o in D : M meets H_o}                 H_o = {alive q : o in t_q}
+      //   same = |M & Eq_p|,  Eq_p = AND over o in D of (o in t_p ? H_o : not H_o)
+      // — |D| column steps per slot instead of a walk over the senders or their classes.
+      int ncls = 0, ncols = 0;
+      uint32_t cls = 0xFFFFu;
+      Mask<W> rem = act, D = mzero<W>();
+      bool cols = false;
+      if (!closed) {
+        Mask<W> il, ul;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          il.w[w] = ~0ull;
+          ul.w[w] = 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          const bool s = (act.w[j] >> P.lane) & 1ull;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            il.w[w] &= s ? t[j].w[w] : ~0ull;
+            ul.w[w] |= s ? t[j].w[w] : 0ull;
+          }
+        }
+        Mask<W> I, U;
+        pk_and_or<W>(il, ul, I, U);
+        D = mandn(U, I);
+        ncols = mpopc(D);
+        cols = ncols <= KsPk<W>::kCols;
+      }
+      if (cols) {
+        Mask<W> dd = D;
+        for (int c = 0; c < ncols; ++c) {
+          const int o = mtake_first(dd);
+          uint32_t hb[W];
+#pragma unroll
+          for (int j = 0; j < W; ++j) hb[j] = mtest(t[j], o) ? 1u : 0u;
+          const Mask<W> H = mand(P.ballot(hb), act);
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            if (P.lane == w) L.hol[c][w] = H.w[w];
+        }
+        lds_sync<1>();
+      } else if (!closed) {
+        for (; ncls < KsPk<W>::kClasses && many(rem); ++ncls) {
+          const Mask<W> tq = load_t<W, 64 * W>(L.ts, mfirst(rem));
+          uint32_t mine[W];
+#pragma unroll
+          for (int jj = 0; jj < W; ++jj) {
+            mine[jj] = meq(t[jj], tq) ? 1u : 0u;
+            if (mine[jj] && ((cls >> (4 * jj)) & 15u) == 15u) cls = (cls & ~(15u << (4 * jj))) | ((uint32_t)ncls << (4 * jj));
+          }
+          const Mask<W> E = mand(P.ballot(mine), rem);
+          rem = mandn(rem, E);
+          if (P.lane < W) {  // uniform values: lane w stores word w
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+              if (P.lane == w) {
+                L.ct[ncls][w] = tq.w[w];
+                L.ce[ncls][w] = E.w[w];
+              }
+          }
+        }
+        lds_sync<1>();
+      }
+      pt.mark(1);
+      // one slot at a time (its HO set M, its merge or adoption)
 #pragma unroll
       for (int j = 0; j < W; ++j) {
-        tnew[j] = t[j];
-        becomeDec[j] = 0;
+        uint32_t becomeDec = 0;
         const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
         const uint32_t live = P.val[j] & (1u - halted[j]) & (1u - decider[j]);
         const uint32_t hc = many(mand(M, Dm)) ? 1u : 0u;
         const uint32_t adopt = live & hc, mergep = live & (1u - hc);
+        Mask<W> tnew = t[j];
         if (pk_any(mergep)) {
-          // same = mailbox.filter(_._2._2 == t).size; uni = t ++ every received t, by classes
-          // of equal t among the alive senders (kset_body)
-          constexpr int kClasses = 8;
           int same = 0;
           Mask<W> uni = t[j];
-          Mask<W> rem = act;
           if (closed) {
             same = ((M.w[j] >> P.lane) & 1ull) ? 1 : 0;
             uni = mor(t[j], M);
-            rem = mzero<W>();
-          }
-          for (int cls = 0; cls < kClasses && many(rem); ++cls) {
-            const Mask<W> tq = load_t<W, 64 * W>(L.ts, mfirst(rem));
-            uint32_t mine[W];
+          } else if (cols) {
+            Mask<W> Eq = act, dd = D;
+            for (int c = 0; c < ncols; ++c) {
+              const int o = mtake_first(dd);
+              Mask<W> H;
 #pragma unroll
-            for (int jj = 0; jj < W; ++jj) mine[jj] = meq(t[jj], tq) ? 1u : 0u;
-            const Mask<W> E = mand(P.ballot(mine), rem);
-            rem = mandn(rem, E);
-            const Mask<W> ME = mand(M, E);
-            if (mine[j]) same = mpopc(ME);
-            if (many(ME)) uni = mor(uni, tq);
-          }
-          while (many(rem)) {
-            const int q = mtake_first(rem);
-            const Mask<W> tq = load_t<W, 64 * W>(L.ts, q);
-            if (mtest(M, q)) {
-              same += meq(tq, t[j]) ? 1 : 0;
-              uni = mor(uni, tq);
+              for (int w = 0; w < W; ++w) H.w[w] = L.hol[c][w];
+              const bool hit = many(mand(M, H));
+              const uint64_t bit = 1ull << (o & 63);
+              const bool mine = mtest(t[j], o);
+#pragma unroll
+              for (int w = 0; w < W; ++w) {
+                uni.w[w] |= (hit && (o >> 6) == w) ? bit : 0ull;
+                Eq.w[w] &= mine ? H.w[w] : ~H.w[w];
+              }
+            }
+            same = mpopc(mand(M, Eq));
+          } else {
+            const int mc = (int)((cls >> (4 * j)) & 15u);
+            for (int c = 0; c < ncls; ++c) {
+              Mask<W> E, tq;
+#pragma unroll
+              for (int w = 0; w < W; ++w) {
+                E.w[w] = L.ce[c][w];
+                tq.w[w] = L.ct[c][w];
+              }
+              const Mask<W> ME = mand(M, E);
+              if (c == mc) same = mpopc(ME);
+              if (many(ME)) uni = mor(uni, tq);
+            }
+            Mask<W> rr = rem;
+            while (many(rr)) {
+              const int q = mtake_first(rr);
+              const Mask<W> tq = load_t<W, 64 * W>(L.ts, q);
+              if (mtest(M, q)) {
+                same += meq(tq, t[j]) ? 1 : 0;
+                uni = mor(uni, tq);
+              }
             }
           }
           if (mergep) {
-            if (same > need) becomeDec[j] = 1;
-            else tnew[j] = uni;
+            if (same > need) becomeDec = 1;
+            else tnew = uni;
           }
         }
         if (adopt) {  // t = content.find(_._1).get._2 — first decider message in iteration order
-          tnew[j] = load_t<W, 64 * W>(L.ts, kset_find<W, 64 * W>(a, L.ts, M, mand(M, Dm)));
-          becomeDec[j] = 1;
+          tnew = load_t<W, 64 * W>(L.ts, kset_find<W, 64 * W>(a, L.ts, M, mand(M, Dm), cols ? L.hol : nullptr, ncols));
+          becomeDec = 1;
         }
         if (!halted[j] && decider[j]) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:48-50)
           const int32_t v = kset_pick<W>(t[j], L.x0s, Emin, xmin);
@@ -246,27 +367,30 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
           decision[j] = v;
           halt_round[j] = k;
         }
+        if (!halted[j]) {  // the post-round state of slot j (its pre-round t is in the staging)
+          t[j] = tnew;
+          decider[j] |= becomeDec;
+        }
       }
       lds_sync<1>();  // all reads of ts done before the next round restages it
       uint32_t al[W];
 #pragma unroll
       for (int j = 0; j < W; ++j) {
-        if (!halted[j]) {
-          t[j] = tnew[j];
-          decider[j] |= becomeDec[j];
-        }
         if (halt_round[j] == k) halted[j] = 1;
         al[j] = P.val[j] & (1u - halted[j]);
       }
       act = P.ballot(al);
+      pt.mark(2);
     }
     check(k + 1);
+    pt.mark(4);
   }
   int32_t mainx[W];
 #pragma unroll
   for (int j = 0; j < W; ++j) mainx[j] = P.val[j] ? kset_pick<W>(t[j], L.x0s, Emin, xmin) : 0;
   pk_finish<W>(P, a, i, ck, 2, dec_val, dec_round, halt_round, mainx, bc);
   lds_sync<1>();  // x0s / ts reads done before the next instance restages them
+  pt.mark(3);
 }
 
 #ifndef PSG_KSET_PK_WPE
@@ -282,11 +406,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_KS
   Pk<W> P;
   P.setup(a.n);
   const int grp = threadIdx.x >> 6;
+  PhaseTimers pt;  // profiling builds only: t0 setup, t1 staging + classes, t2 slot updates, t3 finish,
+  pt.start();      // t4 check after a live round, t5 frozen round
   InstanceQueue<1> Q;
   for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
-    kset_packed<W>(P, a, i, inst, L[grp], x0tab[grp], &bc);
+    kset_packed<W>(P, a, i, inst, L[grp], x0tab[grp], &bc, pt);
   }
+  pt.flush(a.counters, P.lane);
   __syncthreads();
   counters_flush(&bc, a.counters, 2, a.R);
 }

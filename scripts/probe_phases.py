@@ -18,6 +18,10 @@ elif which == "benor":
     runs = [(psync.BenOr(), 128, 64, 1_000_000, {}, "C5 BenOr")]
 elif which == "fm":
     runs = [(psync.FloodMin(f), 256, f + 2, 1_000_000, {}, f"FloodMin f={f}") for f in (0, 8)]
+elif which == "kset4":  # the C4 KSet rows' schedule (bench_configs.py)
+    runs = [(psync.KSetAgreement(2), 256, 16, 200_000,
+             dict(schedule=psync.HOSchedule(drop_log2=0, good_round=0.0, crash_fmax=f)), f"KSet C4 f={f}")
+            for f in (1, 32)]
 else:
     runs = [(psync.KSetAgreement(2), 256, 16, 200_000, {}, "KSet k=2")]
 for alg, n, R, I, kw, label in runs:
