@@ -178,7 +178,10 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
   const Mask<W> Emin = P.ballot(emin);
   Checks ck;
   ck.reset();
-  auto check = [&](int c) { pk_kagree_check<W>(P, ck, c, kk, decided, decision, cr, X0); };
+  uint32_t notinit[W];  // X0 probe of each slot's decision, taken when it decides (pk_kagree_check_m)
+#pragma unroll
+  for (int j = 0; j < W; ++j) notinit[j] = 0;
+  auto check = [&](int c) { pk_kagree_check_m<W>(P, ck, c, kk, decided, decision, cr, notinit); };
   check(0);
   pt.mark(0);
   Mask<W> act;
@@ -189,12 +192,10 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
     act = P.ballot(al);
   }
   for (int k = 0; k < a.R; ++k) {
-    // Every process halted: the state is frozen from here on, and the k-agreement predicate
-    // reads only (decided, decision, crashed, X0) — no round counter — so check points
-    // k+1 .. R evaluate to check point k's result, already recorded (first-failure and
-    // termination are running minima): they are resolved without re-evaluation.
-    if (!many(act)) break;
-    {
+    // Once every process halted the state is frozen; the round has no step to take, but its
+    // check point is still evaluated (every counted process-round is checked).
+    const bool live = many(act);
+    if (live) {
       Mask<W> goodS;
       const bool good = sc.good_round(k, P.lane, a.R, goodS);
       Mask<W> CB = mzero<W>(), CN = mzero<W>();
@@ -365,6 +366,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
           dec_round[j] = k;
           decided[j] = 1;
           decision[j] = v;
+          notinit[j] = 1u - X0.contains01(v);
           halt_round[j] = k;
         }
         if (!halted[j]) {  // the post-round state of slot j (its pre-round t is in the staging)
@@ -383,7 +385,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
       pt.mark(2);
     }
     check(k + 1);
-    pt.mark(4);
+    pt.mark(live ? 4 : 5);
   }
   int32_t mainx[W];
 #pragma unroll

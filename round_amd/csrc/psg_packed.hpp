@@ -113,16 +113,18 @@ PSG_DEV void pk_x0_build(const Pk<W>& P, X0Set<W>& X, int32_t* lds, const int32_
 
 // k-agreement over a packed instance (kagree_check): slot 0 — the decisions of never-
 // crashed deciders number <= k; slot 1 — every decision is an initial value; termination
-// when every process decided.
+// when every process decided. notinit: per slot, "decided and its decision is not an initial
+// value" — the X0 probe of a decision, taken by the caller when the decision is made (a
+// decision never changes afterwards), or here (pk_kagree_check).
 template <int W>
-PSG_DEV void pk_kagree_check(const Pk<W>& P, Checks& ck, int c, int kk, const uint32_t (&decided)[W],
-                             const int32_t (&decision)[W], const int32_t (&cr)[W], const X0Set<W>& X0) {
+PSG_DEV void pk_kagree_check_m(const Pk<W>& P, Checks& ck, int c, int kk, const uint32_t (&decided)[W],
+                               const int32_t (&decision)[W], const int32_t (&cr)[W], const uint32_t (&notinit)[W]) {
   uint32_t dc[W], undec = 0, bad = 0;
 #pragma unroll
   for (int j = 0; j < W; ++j) {
     dc[j] = P.val[j] & decided[j] & (cr[j] >= 0 ? 0u : 1u);
     undec |= P.val[j] & (1u - decided[j]);
-    bad |= P.val[j] & decided[j] & (1u - X0.contains01(decision[j]));
+    bad |= P.val[j] & decided[j] & notinit[j];
   }
   Mask<W> Y = P.ballot(dc);
   int distinct = 0;
@@ -135,6 +137,15 @@ PSG_DEV void pk_kagree_check(const Pk<W>& P, Checks& ck, int c, int kk, const ui
     ++distinct;
   }
   ck.record(fbit(distinct <= kk, 0) | fbit(!pk_any(bad), 1), !pk_any(undec), c, P.lane);
+}
+
+template <int W>
+PSG_DEV void pk_kagree_check(const Pk<W>& P, Checks& ck, int c, int kk, const uint32_t (&decided)[W],
+                             const int32_t (&decision)[W], const int32_t (&cr)[W], const X0Set<W>& X0) {
+  uint32_t notinit[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) notinit[j] = 1u - X0.contains01(decision[j]);
+  pk_kagree_check_m<W>(P, ck, c, kk, decided, decision, cr, notinit);
 }
 
 // Per-instance epilogue of a packed instance (finish_instance for W slots per lane):

@@ -109,6 +109,25 @@ bool tuple_fields(const Tree& T, int q, std::vector<std::pair<int, int>>& out) {
   return out.size() <= 4;
 }
 
+// Does the body of process quantifier q read its variable only through current / old fields
+// (no init field, no use as a pid)? (formula.py _symmetric)
+bool symmetric(const Tree& T, int q) {
+  const int uid = T.nodes[q].uid;
+  std::vector<int> w;
+  T.walk(T.nodes[q].a, w);
+  int nvar = 0, nfield = 0;
+  for (int x : w) {
+    const Node& n = T.nodes[x];
+    if (n.k == VAR && n.uid == uid) {
+      ++nvar;
+    } else if (n.k == FIELD && is_var(T, n.a, uid)) {
+      if (n.tag == PSG_TAG_INIT) return false;
+      ++nfield;
+    }
+  }
+  return nvar == nfield;
+}
+
 // breakpoint offsets (bit d+1: b = e + d) of an atom `t OP e`, t the V.exists variable
 int bp_shift(int op) {
   switch (op) {
@@ -350,6 +369,10 @@ struct Gen {
   std::vector<std::pair<std::vector<std::pair<int, int>>, std::string>> tup_sets;
   std::set<std::vector<std::pair<int, int>>> tup_used;
   std::map<std::pair<int, int>, int> memo_slots;
+  bool uni = false;                          // lowering for symmetric check points (spec::uniform)
+  std::set<int> pvars;                       // variables bound to a process (a pid in [0, n))
+  std::vector<std::pair<int, int>> uft;      // (field, tag) current / old fields the symmetric lowering reads
+  std::map<std::pair<int, std::string>, int> umemo;  // (init set, C++ expression) -> member_init_u slot
 
   bool own(int uid) const {
     auto it = names.find(uid);
@@ -360,6 +383,9 @@ struct Gen {
       throw SpecError("field " + S(f) + " is not part of this algorithm's state");
   }
   std::string next(const char* p) { return p + S(k++); }
+  void add_uft(int f, int tag) {
+    if (std::find(uft.begin(), uft.end(), std::make_pair(f, tag)) == uft.end()) uft.emplace_back(f, tag);
+  }
 
   Code gen(int e, bool in_lane, int vi) {
     auto c = cse.find(e);
@@ -380,6 +406,13 @@ struct Gen {
         fields.insert(n.f);
         tags.insert(n.tag);
         const Node& p = T.nodes[n.a];
+        if (uni && n.tag != PSG_TAG_INIT) {
+          // symmetric check point: every process holds process 0's value
+          add_uft(n.f, n.tag);
+          if (p.k == COORDV || (p.k == VAR && pvars.count(p.uid))) return {"x.uf(" + S(n.tag) + ", " + S(n.f) + ")", false};
+          const Code pc = gen(n.a, in_lane, vi);
+          return {"spec::fld_uni<W>(x, " + S(n.tag) + ", " + S(n.f) + ", " + pc.first + ")", pc.second};
+        }
         if (p.k == VAR && own(p.uid)) return {"x.own(" + S(n.tag) + ", " + S(n.f) + ")", true};  // the lane's own process
         if (p.k == VAR && tuples.count(p.uid)) return {tuples[p.uid][{n.f, n.tag}], false};  // a distinct-state tuple value
         const Code pc = gen(n.a, in_lane, vi);
@@ -415,6 +448,8 @@ struct Gen {
         const Code val = gen(n.a, in_lane, vi);
         const std::string v = next("b");
         const bool own_e = T.nodes[n.a].k == VAR && own(T.nodes[n.a].uid);
+        if (T.nodes[n.a].k == COORDV || (T.nodes[n.a].k == VAR && pvars.count(T.nodes[n.a].uid)))
+          pvars.insert(n.uid);  // a process's pid
         // A.contains(i) for the lane's own process i: the comprehension's variable is that
         // process too (its fields are the lane's registers, not a gather)
         names[n.uid] = own_e ? Name{val.first, true, true} : Name{v, val.second, false};
@@ -456,6 +491,11 @@ struct Gen {
     const std::string v = next("v");
     if (Q.qk == QFORALL || Q.qk == QEXISTS || Q.qk == QCOUNT) {
       const int mode = Q.qk == QFORALL ? 0 : Q.qk == QEXISTS ? 1 : 2;
+      pvars.insert(Q.uid);
+      if (uni) {
+        Code got;
+        if (quant_uni(q, v, in_lane, vi, got)) return got;
+      }
       if (!in_lane) {
         names[Q.uid] = Name{v, true, true};
         const Code body = gen(Q.a, true, vi);
@@ -535,10 +575,20 @@ struct Gen {
       // none active, the finitization below decides it
       const std::string pl = next("p");
       names[T.nodes[P.forall].uid] = Name{pl, true, true};
+      pvars.insert(T.nodes[P.forall].uid);
       std::vector<std::string> conds, vals;
+      bool plane = false;
       for (auto& ct : P.list) {
-        conds.push_back(ct.first < 0 ? "1" : "(int32_t)((" + gen(ct.first, true, vi).first + ") != 0)");
-        vals.push_back(gen(ct.second, true, vi).first);
+        if (ct.first < 0) {
+          conds.push_back("1");
+        } else {
+          const Code cc = gen(ct.first, true, vi);
+          conds.push_back("(int32_t)((" + cc.first + ") != 0)");
+          plane = plane || cc.second;
+        }
+        const Code tc = gen(ct.second, true, vi);
+        vals.push_back(tc.first);
+        plane = plane || tc.second;
       }
       std::string act;
       for (size_t i = 0; i < conds.size(); ++i) act += (i ? " | " : "") + conds[i];
@@ -549,12 +599,59 @@ struct Gen {
       names[Q.uid] = Name{v, false, false};
       const Code body = gen(Q.a, in_lane, vi + 1);
       max_vi = std::max(max_vi, vi + 1);
+      if (uni && !plane)  // symmetric check point: every process has the same pin flag and value
+        return {"spec::pin_uni(" + act + ", " + val + ", " + lam("int32_t " + v, body.first) +
+                    ", [&]() -> int32_t { return " + general.first + "; })",
+                body.second || general.second};
       return {"spec::exists_int_pin<W>(x, " + lam("int32_t " + pl, act) + ", " + lam("int32_t " + pl, val) +
                   ", scratch + " + S(vi) + " * 64 * W, " + lam("int32_t " + v, body.first) +
                   ", [&]() -> int32_t { return " + general.first + "; })",
               true};
     }
     return vint_unpinned(q, v, in_lane, vi);
+  }
+
+  // A process quantifier on a symmetric check point (formula.py _quant_uni), false for the
+  // general rules: a body reading its variable only through current / old fields has one value
+  // for every process; P.exists(j => init(j.f) == t) with a group-uniform t is a scalar-memoized probe
+  bool quant_uni(int q, const std::string& v, bool in_lane, int vi, Code& out) {
+    const Node Q = T.nodes[q];
+    const int mode = Q.qk == QFORALL ? 0 : Q.qk == QEXISTS ? 1 : 2;
+    if (symmetric(T, q)) {
+      names[Q.uid] = Name{"0", false, false};  // never read but through its fields
+      const Code body = gen(Q.a, in_lane, vi);
+      if (body.second && !in_lane) {
+        // a group-uniform value in a lane register: reduced over the valid lanes
+        const char* fn = mode == 0 ? "forall_lane" : mode == 1 ? "exists_lane" : "count_lane";
+        out = {std::string("spec::") + fn + "<W>(x, " + lam("int32_t " + v, body.first) + ")", false};
+        return true;
+      }
+      if (mode == 2) out = {"((" + body.first + ") != 0 ? x.n : 0)", body.second};
+      else out = {"(int32_t)((" + body.first + ") != 0)", body.second};
+      return true;
+    }
+    const std::pair<int, int> mem = init_member(T, q);
+    if (mem.first >= 0 && (std::find(init_sets.begin(), init_sets.end(), mem.first) != init_sets.end() ||
+                           init_sets.size() < 2)) {
+      const int f = mem.first;
+      const Code tc = gen(mem.second, in_lane, vi);
+      if (tc.second) return false;
+      if (std::find(init_sets.begin(), init_sets.end(), f) == init_sets.end()) init_sets.push_back(f);
+      fields.insert(f);
+      tags.insert(PSG_TAG_INIT);
+      const int K = (int)(std::find(init_sets.begin(), init_sets.end(), f) - init_sets.begin());
+      const std::pair<int, std::string> key{K, tc.first};
+      if (!umemo.count(key) && umemo.size() < 4) {
+        const int slot = (int)umemo.size();
+        umemo[key] = slot;
+      }
+      if (umemo.count(key))
+        out = {"spec::member_init_u<W, " + S(K) + ", " + S(umemo[key]) + ">(x, " + tc.first + ")", false};
+      else
+        out = {"spec::member_init<W, " + S(K) + ">(x, " + tc.first + ")", false};
+      return true;
+    }
+    return false;
   }
 
   // V.exists over Int: count-guarded candidates, else the general finitization
@@ -579,6 +676,14 @@ struct Gen {
       names[uid] = Name{v, false, false};
       const Code body = gen(T.nodes[q].a, in_lane, vi + 1);
       max_vi = std::max(max_vi, vi + 1);
+      if (uni && g.tag != PSG_TAG_INIT) {
+        // symmetric check point: process 0's value is the only one, held by n processes
+        add_uft(g.f, g.tag);
+        return {"([&]() -> int32_t { const int32_t L_ = " + L + "; if (L_ >= 1) return spec::guard_uni<W>(x, x.uf(" +
+                    S(g.tag) + ", " + S(g.f) + "), L_, " + lam("int32_t " + v, body.first) + "); return " +
+                    general.first + "; })()",
+                body.second || general.second};
+      }
       return {"([&]() -> int32_t { const int32_t L_ = " + L + "; if (L_ >= 1) return spec::exists_int_guard<W, " +
                   S(g.f | (g.tag << 8)) + ">(x, x.own(" + S(g.tag) + ", " + S(g.f) + "), x.stage(" + S(g.tag) + ", " +
                   S(g.f) + "), L_, " + lam("int32_t " + v, body.first) + "); return " + general.first + "; })()",
@@ -602,6 +707,9 @@ struct Gen {
     }
     max_vi = std::max(max_vi, vi + 1);
     const Code body = gen(T.nodes[q].a, in_lane, vi + 1);
+    // its value is group-uniform outside a lane quantifier (the candidates are); the general
+    // lowering keeps the conservative lane flag
+    const bool vlane = uni ? (in_lane || body.second) : true;
     const int ne = (int)evs.size(), nf = (int)fsets.size();
     std::string ev, fs;
     for (int i = 0; i < ne; ++i) ev += (i ? ", " : "") + evs[i];
@@ -614,7 +722,7 @@ struct Gen {
     if (eqo)
       return {head + "return spec::exists_int_eq<W, " + S(ne) + ", " + S(nf) + ">(x, ev_, fs_, scratch + " + S(vi) +
                   " * 64 * W, " + tail,
-              true};
+              vlane};
     // order comparisons: one candidate per breakpoint (exists_int_bp) instead of v-1, v, v+1
     const std::vector<int> sh = breakpoint_shifts(T, q, exprs, fsets);
     std::string shs;
@@ -622,7 +730,7 @@ struct Gen {
     if (shs.empty()) shs = "0u";
     return {head + "const uint32_t sh_[" + S(std::max(ne + nf, 1)) + "] = {" + shs + "}; return spec::exists_int_bp<W, " +
                 S(ne) + ", " + S(nf) + ">(x, ev_, fs_, sh_, scratch + " + S(vi) + " * 64 * W, " + tail,
-            true};
+            vlane};
   }
 };
 
@@ -636,8 +744,6 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
   std::vector<std::pair<std::string, int>> props;
   for (auto& p : P.props) props.emplace_back(p.first, rewrite_vint(T, p.second, memo));
   const int safety = P.sp < 0 ? -1 : rewrite_vint(T, P.sp, memo);
-  std::vector<std::string> lines;
-  int slot = 0;
   // common closed subformulas (the same node under several slots): hoisted, evaluated once per check point
   std::vector<int> roots = invs;
   for (auto& p : props)
@@ -657,66 +763,112 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
     };
     V::visit(T, rt, seen, order);
   }
-  for (int e : order) {
-    const Kind kd = T.nodes[e].k;
-    if (seen[e] > 1 && (kd == QUANT || kd == CONTAINS) && free_of(T, e).empty()) {
-      const Code c = gen.gen(e, false, 0);
-      const std::string name = "cse" + S((int)gen.cse.size());
-      lines.push_back("    const int32_t " + name + " = " + c.first + ";");
-      gen.cse[e] = name;
-    }
-  }
-  if (!invs.empty()) {
-    for (size_t k = 0; k < invs.size(); ++k) {
-      const Code c = gen.gen(invs[k], false, 0);
-      lines.push_back("    const int32_t inv" + S((int)k) + " = " + c.first + ";");
-    }
-    std::string any;
-    for (size_t k = 0; k < invs.size(); ++k) any += (k ? " | " : "") + std::string("(inv") + S((int)k) + " != 0)";
-    lines.push_back("    if (!(" + any + ")) fb |= 1u << " + S(slot) + ";");
-    ++slot;
-    for (size_t k = 0; k < invs.size(); ++k) {
-      lines.push_back("    if (inv" + S((int)k) + " == 0) fb |= 1u << " + S(slot) + ";");
-      ++slot;
-    }
-  }
-  std::string term;
-  bool has_term = false;
-  std::set<std::vector<std::pair<int, int>>> term_tups;
-  for (auto& p : props) {
-    if (p.first == "Termination") {
-      auto saved = gen.tup_used;
-      gen.tup_used.clear();
-      term = gen.gen(p.second, false, 0).first;
-      has_term = true;
-      term_tups = gen.tup_used;
-      gen.tup_used = saved;
-      continue;
-    }
-    const Code c = gen.gen(p.second, false, 0);
-    lines.push_back("    if ((" + c.first + ") == 0) fb |= 1u << " + S(slot) + ";  // " + p.first);
-    ++slot;
-  }
-  if (safety >= 0) {
-    const Code c = gen.gen(safety, false, 0);
-    lines.push_back("    if ((" + c.first + ") == 0) fb |= 1u << " + S(slot) + ";  // SafetyPredicate");
-    ++slot;
-  }
-  if (slot != (int)prog.entry.size()) throw SpecError("native lowering: slot count mismatch");
-  if (gen.max_vi > 4) throw SpecError("more than 4 nested V.exists over Int");
-  auto tup_decls = [&](const std::set<std::vector<std::pair<int, int>>>& used) {
+  auto tup_decls = [&](const std::set<std::vector<std::pair<int, int>>>& used, const std::string& ind) {
     std::vector<std::string> out;
     for (auto& ts : gen.tup_sets) {
       if (!used.count(ts.first)) continue;
       std::string fl;
       for (size_t i = 0; i < ts.first.size(); ++i)
         fl += (i ? ", " : "") + std::string("spec::Fld<") + S(ts.first[i].first) + ", " + S(ts.first[i].second) + ">{}";
-      out.push_back("    const auto " + ts.second + " = spec::tup_uniform<W>(x, " + fl + ");");
+      out.push_back(ind + "const auto " + ts.second + " = spec::tup_uniform<W>(x, " + fl + ");");
     }
     return out;
   };
-  std::vector<std::string> body = tup_decls(gen.tup_used);
-  body.insert(body.end(), lines.begin(), lines.end());
+  struct Block {
+    std::vector<std::string> lines, term_decls;
+    std::string term;
+    bool has_term = false;
+    int slot = 0;
+  };
+  // the slot lines of fail() and the Termination expression, under the general or the
+  // symmetric-check-point lowering (formula.py codegen_hip block)
+  auto block = [&](bool uni) {
+    gen.uni = uni;
+    gen.cse.clear();
+    gen.tup_used.clear();
+    const std::string ind = uni ? "      " : "    ", pre = uni ? "ucse" : "cse", iv = uni ? "uinv" : "inv";
+    Block B;
+    std::vector<std::string> lines;
+    int slot = 0;
+    for (int e : order) {
+      const Kind kd = T.nodes[e].k;
+      if (seen[e] > 1 && (kd == QUANT || kd == CONTAINS) && free_of(T, e).empty()) {
+        const Code c = gen.gen(e, false, 0);
+        const std::string name = pre + S((int)gen.cse.size());
+        lines.push_back(ind + "const int32_t " + name + " = " + c.first + ";");
+        gen.cse[e] = name;
+      }
+    }
+    if (!invs.empty()) {
+      for (size_t k = 0; k < invs.size(); ++k) {
+        const Code c = gen.gen(invs[k], false, 0);
+        lines.push_back(ind + "const int32_t " + iv + S((int)k) + " = " + c.first + ";");
+      }
+      std::string any;
+      for (size_t k = 0; k < invs.size(); ++k) any += (k ? " | " : "") + std::string("(") + iv + S((int)k) + " != 0)";
+      lines.push_back(ind + "if (!(" + any + ")) fb |= 1u << " + S(slot) + ";");
+      ++slot;
+      for (size_t k = 0; k < invs.size(); ++k) {
+        lines.push_back(ind + "if (" + iv + S((int)k) + " == 0) fb |= 1u << " + S(slot) + ";");
+        ++slot;
+      }
+    }
+    std::set<std::vector<std::pair<int, int>>> term_tups;
+    for (auto& p : props) {
+      if (p.first == "Termination") {
+        auto saved = gen.tup_used;
+        gen.tup_used.clear();
+        B.term = gen.gen(p.second, false, 0).first;
+        B.has_term = true;
+        term_tups = gen.tup_used;
+        gen.tup_used = saved;
+        continue;
+      }
+      const Code c = gen.gen(p.second, false, 0);
+      lines.push_back(ind + "if ((" + c.first + ") == 0) fb |= 1u << " + S(slot) + ";  // " + p.first);
+      ++slot;
+    }
+    if (safety >= 0) {
+      const Code c = gen.gen(safety, false, 0);
+      lines.push_back(ind + "if ((" + c.first + ") == 0) fb |= 1u << " + S(slot) + ";  // SafetyPredicate");
+      ++slot;
+    }
+    if (slot != (int)prog.entry.size()) throw SpecError("native lowering: slot count mismatch");
+    B.lines = tup_decls(gen.tup_used, ind);
+    B.lines.insert(B.lines.end(), lines.begin(), lines.end());
+    B.term_decls = tup_decls(term_tups, ind);
+    B.slot = slot;
+    return B;
+  };
+  Block G = block(false);
+  // symmetric check points (every process holds the same value of each current / old field the
+  // Spec reads): a second, scalar lowering, chosen per check point by spec::uniform
+  Block U = block(true);
+  gen.uni = false;
+  const int slot = G.slot;
+  const bool has_term = G.has_term && !G.term.empty();
+  const std::string term = G.term;
+  std::vector<std::string> body, term_decls;
+  if (!gen.uft.empty()) {
+    uint32_t cur = 0, old = 0;
+    for (auto& ft : gen.uft) {
+      if (ft.second == PSG_TAG_CUR) cur |= 1u << ft.first;
+      else if (ft.second == PSG_TAG_OLD) old |= 1u << ft.first;
+    }
+    body.push_back("    if (spec::uniform<W, " + std::to_string(cur) + "u, " + std::to_string(old) + "u>(x)) {");
+    body.insert(body.end(), U.lines.begin(), U.lines.end());
+    body.push_back("      return fb;");
+    body.push_back("    }");
+    if (has_term) {
+      term_decls.push_back("    if (x.uni) {");
+      term_decls.insert(term_decls.end(), U.term_decls.begin(), U.term_decls.end());
+      term_decls.push_back("      return (" + U.term + ") != 0;");
+      term_decls.push_back("    }");
+    }
+  }
+  body.insert(body.end(), G.lines.begin(), G.lines.end());
+  term_decls.insert(term_decls.end(), G.term_decls.begin(), G.term_decls.end());
+  if (gen.max_vi > 4) throw SpecError("more than 4 nested V.exists over Int");
   uint32_t rel = 0, fmask = 0, tmask = 0;
   for (size_t s = 0; s < prog.flags.size(); ++s)
     if (prog.flags[s] & PSG_SPEC_RELATIONAL) rel |= 1u << s;
@@ -744,7 +896,7 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
     << "  template <int W>\n"
     << "  __device__ static bool term(spec::Ctx<W>& x, int32_t* scratch) {\n"
     << "    (void)scratch;\n";
-  for (auto& l : tup_decls(term_tups)) o << l << "\n";
+  for (auto& l : term_decls) o << l << "\n";
   o << "    return (" << (has_term && !term.empty() ? term : "0") << ") != 0;\n"
     << "  }\n"
     << "};\n"

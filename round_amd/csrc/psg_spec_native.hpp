@@ -41,9 +41,61 @@ struct Ctx {
   // (valid once bit M of mok is set; a Ctx lives for one instance)
   uint32_t mok = 0;
   int32_t mv[4] = {0, 0, 0, 0}, mr[4] = {0, 0, 0, 0};
+  // symmetric check point (uniform<>): every process holds the same current / old value of each
+  // field the uniform lowering reads, process 0's in uc / uo; uni says whether it holds
+  bool uni = false;
+  int32_t uc[PSG_NFIELDS] = {0}, uo[PSG_NFIELDS] = {0};
+  // member_init_u: per memo slot, the last probed (uniform) value and its membership
+  uint32_t muok = 0;
+  int32_t muv[4] = {0, 0, 0, 0}, mur[4] = {0, 0, 0, 0};
   PSG_DEV const int32_t* stage(int tag, int f) const { return sc + (tag * PSG_NFIELDS + f) * 64 * W; }
   PSG_DEV int32_t own(int tag, int f) const { return tag == PSG_TAG_CUR ? c[f] : (tag == PSG_TAG_OLD ? o[f] : i[f]); }
+  PSG_DEV int32_t uf(int tag, int f) const { return tag == PSG_TAG_CUR ? uc[f] : uo[f]; }
 };
+
+// ---------------------------------------------------------------- symmetric check points
+// A check point is symmetric for a Spec when every process holds the same value of each
+// current / old field the Spec reads (settled OTR states: all decided on one value). Then a
+// process quantifier whose body reads its variable only through such fields has the same
+// body value for every process: forall / exists give that value, count gives n or 0, and a
+// field of any process is process 0's. The generator emits a second lowering of the Spec
+// under that assumption (scalar code, no ballots for those quantifiers) and this test picks
+// it per check point; it is exact for every state (n >= 1: process 0 exists).
+// The lowest current field is tested alone first: a Spec whose states are rarely symmetric
+// (LastVoting: crashed processes never decide) pays one broadcast and one ballot.
+template <int W, uint32_t CUR, uint32_t OLD>
+PSG_DEV bool uniform(Ctx<W>& x) {
+  constexpr int F0 = CUR ? __builtin_ctz(CUR) : -1;
+  constexpr bool kTwo = F0 >= 0 && ((CUR & (CUR - 1)) | OLD) != 0u;  // more than one field
+  if constexpr (kTwo) {
+    x.uc[F0] = x.g.bcast(x.c[F0], x.stage(PSG_TAG_CUR, F0), 0);
+    if (x.g.any(x.c[F0] != x.uc[F0])) {
+      x.uni = false;
+      return false;
+    }
+  }
+  uint32_t diff = 0;
+#pragma unroll
+  for (int f = 0; f < PSG_NFIELDS; ++f) {
+    if (((CUR >> f) & 1u) && !(kTwo && f == F0)) {
+      x.uc[f] = x.g.bcast(x.c[f], x.stage(PSG_TAG_CUR, f), 0);
+      diff |= ne01(x.c[f], x.uc[f]);
+    }
+    if ((OLD >> f) & 1u) {
+      x.uo[f] = x.g.bcast(x.o[f], x.stage(PSG_TAG_OLD, f), 0);
+      diff |= ne01(x.o[f], x.uo[f]);
+    }
+  }
+  x.uni = !x.g.any(diff != 0u);
+  return x.uni;
+}
+
+// field (tag) of the process with pid q on a symmetric check point (0 for a pid outside
+// [0, n), as fld_u / fld_g)
+template <int W>
+PSG_DEV int32_t fld_uni(Ctx<W>& x, int tag, int f, int32_t q) {
+  return (q >= 0 && q < x.n) ? x.uf(tag, f) : 0;
+}
 
 // field f (state tag) of the uniform process q
 template <int W>
@@ -209,6 +261,18 @@ PSG_DEV int32_t member_init_own(Ctx<W>& x) {
     x.mok |= 1u << M;
   }
   return x.mr[M];
+}
+
+// member_init of a group-uniform value t (symmetric check points): the same memo per slot M as
+// member_init_own, kept in scalar registers; the set is probed only when t changed
+template <int W, int K, int M>
+PSG_DEV int32_t member_init_u(Ctx<W>& x, int32_t t) {
+  if (!((x.muok >> M) & 1u) || t != x.muv[M]) {
+    x.mur[M] = rfl32((int32_t)x.iset[K].contains01(t));
+    x.muv[M] = t;
+    x.muok |= 1u << M;
+  }
+  return x.mur[M];
 }
 
 // ---------------------------------------------------------------- connectives with an expensive right side
@@ -410,6 +474,22 @@ PSG_DEV int32_t exists_int_pin(Ctx<W>& x, FA act, FV val, int32_t* scratch, Fn f
     return fn(v) != 0 ? 1 : 0;
   }
   return general();
+}
+
+// exists_int_pin on a symmetric check point whose pinning process variable reads only
+// symmetric fields: the pin flag and value are the same for every process
+template <class Fn, class Gen>
+PSG_DEV int32_t pin_uni(int32_t act, int32_t val, Fn fn, Gen general) {
+  if (act != 0) return fn(val) != 0 ? 1 : 0;
+  return general();
+}
+
+// exists_int_guard on a symmetric check point: every process holds t = u, so u is the only
+// value held by L >= 1 processes (n of them)
+template <int W, class Fn>
+PSG_DEV int32_t guard_uni(Ctx<W>& x, int32_t u, int32_t L, Fn fn) {
+  if (x.n < L) return 0;
+  return fn(u) != 0 ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- arithmetic with Scala Int semantics

@@ -721,6 +721,10 @@ class _Gen:
         self.tup_sets = {}    # field tuple of a distinct-state quantifier -> C++ name of its per-check-point TupU
         self.tup_used = set()  # field tuples used by the function being generated
         self.memo_slots = {}   # (init set, field) -> memo slot of member_init_own
+        self.uni = False       # lowering for symmetric check points (spec::uniform, psg_spec_native.hpp)
+        self.pvars = set()     # uids of variables bound to a process (a pid in [0, n))
+        self.uft = []          # (field, tag) current / old fields read by the symmetric lowering
+        self.umemo = {}        # (init set, C++ expression) -> memo slot of member_init_u
 
     def gen(self, e, in_lane, vi_depth):
         """(C++ expression, depends on the lane)."""
@@ -744,6 +748,14 @@ class _Gen:
                 raise FormulaError(f"field {e.f} is not part of this algorithm's state")
             self.fields.add(e.f)
             self.tags.add(e.tag)
+            if self.uni and e.tag != TAG_INIT:
+                # symmetric check point: every process holds process 0's value
+                if (e.f, e.tag) not in self.uft:
+                    self.uft.append((e.f, e.tag))
+                if isinstance(e.proc, CoordVal) or (isinstance(e.proc, Var) and e.proc.uid in self.pvars):
+                    return f"x.uf({e.tag}, {e.f})", False
+                p, lane = self.gen(e.proc, in_lane, vi_depth)
+                return f"spec::fld_uni<W>(x, {e.tag}, {e.f}, {p})", lane
             if isinstance(e.proc, Var) and self.names.get(e.proc.uid, (None, False, False))[2]:
                 return f"x.own({e.tag}, {e.f})", True  # the lane's own process
             if isinstance(e.proc, Var) and e.proc.uid in self.tuples:
@@ -775,6 +787,8 @@ class _Gen:
             val, lane = self.gen(e.e, in_lane, vi_depth)
             v = f"b{next(self.k)}"
             own = isinstance(e.e, Var) and self.names.get(e.e.uid, (None, False, False))[2]
+            if isinstance(e.e, CoordVal) or (isinstance(e.e, Var) and e.e.uid in self.pvars):
+                self.pvars.add(e.comp.var.uid)  # a process's pid
             # A.contains(i) for the lane's own process i: the comprehension's variable is that
             # process too (its fields are the lane's registers, not a gather)
             self.names[e.comp.var.uid] = (val, True, True) if own else (v, lane, False)
@@ -787,6 +801,11 @@ class _Gen:
     def quant(self, q, in_lane, vi_depth):
         v = f"v{next(self.k)}"
         if q.kind in ("forall", "exists", "count"):
+            self.pvars.add(q.var.uid)
+            if self.uni:
+                got = self._quant_uni(q, v, in_lane, vi_depth)
+                if got is not None:
+                    return got
             if not in_lane:
                 self.names[q.var.uid] = (v, True, True)
                 body, _ = self.gen(q.body, True, vi_depth)
@@ -852,22 +871,68 @@ class _Gen:
             fq, plist = pins
             pl = f"p{next(self.k)}"
             self.names[fq.var.uid] = (pl, True, True)
-            conds, vals = [], []
+            self.pvars.add(fq.var.uid)
+            conds, vals, plane = [], [], False
             for cond, term in plist:
-                conds.append("1" if cond is None else f"(int32_t)(({self.gen(cond, True, vi_depth)[0]}) != 0)")
-                vals.append(self.gen(term, True, vi_depth)[0])
+                if cond is None:
+                    conds.append("1")
+                else:
+                    cc, cl = self.gen(cond, True, vi_depth)
+                    conds.append(f"(int32_t)(({cc}) != 0)")
+                    plane = plane or cl
+                tc, tl = self.gen(term, True, vi_depth)
+                vals.append(tc)
+                plane = plane or tl
             act = " | ".join(conds)
             val = vals[-1]
             for cc, tc in reversed(list(zip(conds[:-1], vals[:-1]))):
                 val = f"(({cc}) != 0 ? ({tc}) : ({val}))"
-            general, _ = self._vint_unpinned(q, v, in_lane, vi_depth)
+            general, lane_g = self._vint_unpinned(q, v, in_lane, vi_depth)
             self.names[q.var.uid] = (v, False, False)
-            body, _ = self.gen(q.body, in_lane, vi_depth + 1)
+            body, lane_b = self.gen(q.body, in_lane, vi_depth + 1)
             self.max_vi = max(self.max_vi, vi_depth + 1)
+            if self.uni and not plane:
+                # symmetric check point: every process has the same pin flag and value
+                return (f"spec::pin_uni({act}, {val}, [&](int32_t {v}) -> int32_t {{ return {body}; }}, "
+                        f"[&]() -> int32_t {{ return {general}; }})"), lane_b or lane_g
             return (f"spec::exists_int_pin<W>(x, [&](int32_t {pl}) -> int32_t {{ return {act}; }}, "
                     f"[&](int32_t {pl}) -> int32_t {{ return {val}; }}, scratch + {vi_depth} * 64 * W, "
                     f"[&](int32_t {v}) -> int32_t {{ return {body}; }}, [&]() -> int32_t {{ return {general}; }})"), True
         return self._vint_unpinned(q, v, in_lane, vi_depth)
+
+    def _quant_uni(self, q, v, in_lane, vi_depth):
+        """A process quantifier on a symmetric check point, or None for the general rules:
+        a body reading its variable only through current / old fields has one value for every
+        process (forall / exists: that value, count: n or 0); P.exists(j => init(j.f) == t)
+        with a group-uniform t is a scalar-memoized set probe."""
+        if _symmetric(q):
+            self.names[q.var.uid] = ("0", False, False)  # never read but through its fields
+            body, lane = self.gen(q.body, in_lane, vi_depth)
+            if lane and not in_lane:
+                # a group-uniform value in a lane register: reduced over the valid lanes
+                fn = {"forall": "forall_lane", "exists": "exists_lane", "count": "count_lane"}[q.kind]
+                return f"spec::{fn}<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", False
+            if q.kind == "count":
+                return f"(({body}) != 0 ? x.n : 0)", lane
+            return f"(int32_t)(({body}) != 0)", lane
+        mem = _init_member(q)
+        if mem is not None and (mem[0] in self.init_sets or len(self.init_sets) < 2):
+            f, t = mem
+            tc, tl = self.gen(t, in_lane, vi_depth)
+            if tl:
+                return None
+            if f not in self.init_sets:
+                self.init_sets.append(f)
+            self.fields.add(f)
+            self.tags.add(TAG_INIT)
+            K = self.init_sets.index(f)
+            key = (K, tc)
+            if key not in self.umemo and len(self.umemo) < 4:
+                self.umemo[key] = len(self.umemo)
+            if key in self.umemo:
+                return f"spec::member_init_u<W, {K}, {self.umemo[key]}>(x, {tc})", False
+            return f"spec::member_init<W, {K}>(x, {tc})", False
+        return None
 
     def _vint_unpinned(self, q, v, in_lane, vi_depth):
         """V.exists over Int: count-guarded candidates, else the general finitization."""
@@ -888,6 +953,13 @@ class _Gen:
             self.names[q.var.uid] = (v, False, False)
             body, lane = self.gen(q.body, in_lane, vi_depth + 1)
             self.max_vi = max(self.max_vi, vi_depth + 1)
+            if self.uni and tag != TAG_INIT:
+                # symmetric check point: process 0's value is the only one, held by n processes
+                if (f, tag) not in self.uft:
+                    self.uft.append((f, tag))
+                return (f"([&]() -> int32_t {{ const int32_t L_ = {L}; if (L_ >= 1) return "
+                        f"spec::guard_uni<W>(x, x.uf({tag}, {f}), L_, "
+                        f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); return {general}; }})()"), lane or lane_g
             return (f"([&]() -> int32_t {{ const int32_t L_ = {L}; if (L_ >= 1) return "
                     f"spec::exists_int_guard<W, {f | (tag << 8)}>(x, x.own({tag}, {f}), x.stage({tag}, {f}), L_, "
                     f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); return {general}; }})()"), True
@@ -907,6 +979,9 @@ class _Gen:
             self.tags.add(tag)
         self.max_vi = max(self.max_vi, vi_depth + 1)
         body, lane = self.gen(q.body, in_lane, vi_depth + 1)
+        # its value is group-uniform outside a lane quantifier (the candidates are); the general
+        # lowering keeps the conservative lane flag
+        vlane = (in_lane or lane) if self.uni else True
         ne, nf = len(evs), len(fsets)
         ev = ", ".join(evs) if evs else "0"
         fs = ", ".join(str(f | (t << 8)) for f, t in fsets) if fsets else "0"
@@ -915,12 +990,12 @@ class _Gen:
         lam = f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); }})()"
         if eq_only:
             return (head + f"return spec::exists_int_eq<W, {ne}, {nf}>(x, ev_, fs_, scratch + {vi_depth} * 64 * W, "
-                    + lam), True
+                    + lam), vlane
         # order comparisons: one candidate per breakpoint (exists_int_bp) instead of v-1, v, v+1
         sh = _breakpoint_shifts(q, exprs, fsets)
         return (head + f"const uint32_t sh_[{max(ne + nf, 1)}] = {{{', '.join(f'{m}u' for m in sh) or '0u'}}}; "
                 f"return spec::exists_int_bp<W, {ne}, {nf}>(x, ev_, fs_, sh_, scratch + {vi_depth} * 64 * W, "
-                + lam), True
+                + lam), vlane
 
 
 def _expensive(e) -> bool:
@@ -938,6 +1013,21 @@ def _init_member(q):
                 and uid not in {x.uid for x in _walk(b) if isinstance(x, Var)}):
             return a.f, b
     return None
+
+
+def _symmetric(q):
+    """Does the body of process quantifier q read its variable only through current / old
+    fields (no init field, no use as a pid)?"""
+    uid = q.var.uid
+    nvar = nfield = 0
+    for x in _walk(q.body):
+        if isinstance(x, Var) and x.uid == uid:
+            nvar += 1
+        elif isinstance(x, Field) and isinstance(x.proc, Var) and x.proc.uid == uid:
+            if x.tag == TAG_INIT:
+                return False
+            nfield += 1
+    return nvar == nfield
 
 
 def _tuple_fields(q):
@@ -1043,6 +1133,11 @@ def _pins(body, uid, banned=frozenset()):
 SWAP_VINT = False
 
 
+# The symmetric-check-point lowering (spec::uniform); off only for A/B measurements (the C ABI's
+# generator, psg_spec_gen.cpp, always emits it).
+SYMMETRIC_LOWERING = True
+
+
 def _rewrite_vint(e, memo=None):
     """Rewrites of V.exists over Int for the native lowering, exact for every input (the
     domain is non-empty and both sides are decided exactly):
@@ -1121,8 +1216,6 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
     invs = [_rewrite_vint(inv if guard is None else (inv & guard), memo) for inv in spec.invariants]
     props = [(name, _rewrite_vint(f, memo)) for name, f in spec.properties]
     safety = None if spec.safety_predicate is None else _rewrite_vint(spec.safety_predicate, memo)
-    lines = []
-    slot = 0
     # common closed subformulas (the same Formula object used by several slots, e.g.
     # OTR's keepInit in Invariant0 and Invariant1): hoisted, evaluated once per check point
     roots = list(invs) + [f for name, f in props if name != "Termination"]
@@ -1140,44 +1233,69 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
 
     for rt in roots:
         visit(rt)
-    for e in order:
-        if seen[id(e)] > 1 and isinstance(e, (Quant, Contains)) and not _free_vars(e):
-            c, _ = gen.gen(e, False, 0)
-            name = f"cse{len(gen.cse)}"
-            lines.append(f"    const int32_t {name} = {c};")
-            gen.cse[id(e)] = name
-    if invs:
-        for k, inv in enumerate(invs):
-            c, _ = gen.gen(inv, False, 0)
-            lines.append(f"    const int32_t inv{k} = {c};")
-        lines.append("    if (!(" + " | ".join(f"(inv{k} != 0)" for k in range(len(invs))) + f")) fb |= 1u << {slot};")
-        slot += 1
-        for k in range(len(invs)):
-            lines.append(f"    if (inv{k} == 0) fb |= 1u << {slot};")
-            slot += 1
-    term = None
-    term_tups = set()
-    for name, f in props:
-        if name == "Termination":
-            saved, gen.tup_used = gen.tup_used, set()
-            term, _ = gen.gen(f, False, 0)
-            term_tups, gen.tup_used = gen.tup_used, saved
-            continue
-        c, _ = gen.gen(f, False, 0)
-        lines.append(f"    if (({c}) == 0) fb |= 1u << {slot};  // {name}")
-        slot += 1
-    if safety is not None:
-        c, _ = gen.gen(safety, False, 0)
-        lines.append(f"    if (({c}) == 0) fb |= 1u << {slot};  // SafetyPredicate")
-        slot += 1
-    assert slot == len(prog.slot_entry)
-    if gen.max_vi > 4:
-        raise FormulaError("more than 4 nested V.exists over Int")
-    def tup_decls(used):
-        return [f"    const auto {gen.tup_sets[k]} = spec::tup_uniform<W>(x, "
+
+    def tup_decls(used, ind):
+        return [f"{ind}const auto {gen.tup_sets[k]} = spec::tup_uniform<W>(x, "
                 + ", ".join(f"spec::Fld<{f}, {tag}>{{}}" for f, tag in k) + ");"
                 for k in gen.tup_sets if k in used]
-    lines = tup_decls(gen.tup_used) + lines
+
+    def block(uni):
+        """The slot lines of fail() and the Termination expression, under the general or the
+        symmetric-check-point lowering."""
+        gen.uni, gen.cse, gen.tup_used = uni, {}, set()
+        ind, pre = ("      ", "ucse") if uni else ("    ", "cse")
+        lines = []
+        slot = 0
+        for e in order:
+            if seen[id(e)] > 1 and isinstance(e, (Quant, Contains)) and not _free_vars(e):
+                c, _ = gen.gen(e, False, 0)
+                name = f"{pre}{len(gen.cse)}"
+                lines.append(f"{ind}const int32_t {name} = {c};")
+                gen.cse[id(e)] = name
+        iv = "uinv" if uni else "inv"
+        if invs:
+            for k, inv in enumerate(invs):
+                c, _ = gen.gen(inv, False, 0)
+                lines.append(f"{ind}const int32_t {iv}{k} = {c};")
+            lines.append(f"{ind}if (!(" + " | ".join(f"({iv}{k} != 0)" for k in range(len(invs)))
+                         + f")) fb |= 1u << {slot};")
+            slot += 1
+            for k in range(len(invs)):
+                lines.append(f"{ind}if ({iv}{k} == 0) fb |= 1u << {slot};")
+                slot += 1
+        term = None
+        term_tups = set()
+        for name, f in props:
+            if name == "Termination":
+                saved, gen.tup_used = gen.tup_used, set()
+                term, _ = gen.gen(f, False, 0)
+                term_tups, gen.tup_used = gen.tup_used, saved
+                continue
+            c, _ = gen.gen(f, False, 0)
+            lines.append(f"{ind}if (({c}) == 0) fb |= 1u << {slot};  // {name}")
+            slot += 1
+        if safety is not None:
+            c, _ = gen.gen(safety, False, 0)
+            lines.append(f"{ind}if (({c}) == 0) fb |= 1u << {slot};  // SafetyPredicate")
+            slot += 1
+        assert slot == len(prog.slot_entry)
+        return tup_decls(gen.tup_used, ind) + lines, term, tup_decls(term_tups, ind), slot
+
+    lines, term, term_decls, slot = block(False)
+    # symmetric check points (every process holds the same value of each current / old field
+    # the Spec reads): a second, scalar lowering, chosen per check point by spec::uniform
+    ulines, uterm, uterm_decls, _ = block(True)
+    gen.uni = False
+    if gen.uft and SYMMETRIC_LOWERING:
+        cur = sum(1 << f for f, t in gen.uft if t == TAG_CUR)
+        old = sum(1 << f for f, t in gen.uft if t == TAG_OLD)
+        lines = ([f"    if (spec::uniform<W, {cur}u, {old}u>(x)) {{"] + ulines + ["      return fb;", "    }"]
+                 + lines)
+        if term:
+            term_decls = (["    if (x.uni) {"] + uterm_decls + [f"      return ({uterm}) != 0;", "    }"]
+                          + term_decls)
+    if gen.max_vi > 4:
+        raise FormulaError("more than 4 nested V.exists over Int")
     rel = sum(1 << s for s, fl in enumerate(prog.slot_flags) if fl & SPEC_RELATIONAL)
     fmask = sum(1 << f for f in gen.fields)
     tmask = sum(1 << t for t in gen.tags)
@@ -1203,7 +1321,7 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
         "  template <int W>",
         "  __device__ static bool term(spec::Ctx<W>& x, int32_t* scratch) {",
         "    (void)scratch;",
-        *tup_decls(term_tups),
+        *term_decls,
         f"    return ({term or '0'}) != 0;",
         "  }",
         "};",

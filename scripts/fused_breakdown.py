@@ -4,7 +4,8 @@ fused modules that evaluate one formula of OTR.spec at a time (plus an empty Spe
 round kernel alone), kernel time per launch. Compile here (native modules are cached under
 build/spec and travel with the tree), run on the GPU box.
 
-usage: fused_breakdown.py [--compile-only] [--instances N] [--alg otr|lv]
+usage: fused_breakdown.py [--compile-only] [--instances N] [--alg otr|lv] [--nosym]
+(--nosym: modules without the symmetric-check-point lowering, formula.SYMMETRIC_LOWERING)
 """
 import argparse
 import json
@@ -13,6 +14,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from round_amd import abi, formula, psync  # noqa: E402
+from round_amd import formula as F  # noqa: E402
 from round_amd.formula import P, Spec, init, old, true  # noqa: E402
 
 
@@ -45,7 +47,9 @@ def main():
     ap.add_argument("--compile-only", action="store_true")
     ap.add_argument("--instances", type=int, default=2_500_000)
     ap.add_argument("--alg", default="otr")
+    ap.add_argument("--nosym", action="store_true")
     args = ap.parse_args()
+    F.SYMMETRIC_LOWERING = not args.nosym
     if args.alg == "otr":
         alg, aid, kw, variants = psync.OTR(), abi.PSG_ALG_OTR, dict(value_range=64), otr_variants()
     else:
@@ -63,7 +67,7 @@ def main():
         for k, p in progs.items():
             g.run_spec(0, I, p)
             t = [g.run_spec(0, I, p).summary.kernel_ns for _ in range(2)]
-            print(json.dumps({"variant": k, "kernel_ms": min(t) / 1e6}), flush=True)
+            print(json.dumps({"variant": k, "symmetric": not args.nosym, "kernel_ms": min(t) / 1e6}), flush=True)
 
 
 if __name__ == "__main__":

@@ -115,6 +115,25 @@ def order_shapes():
     ])
 
 
+def symmetric_shapes():
+    """Shapes of the symmetric-check-point lowering (spec::uniform: every process holds the
+    same current / old fields): counts of symmetric bodies, old fields, a process used as a
+    pid (Contains) or read through init (not symmetric), quantifiers nested in both orders,
+    coord's fields, and pins / count guards decided by process 0's value."""
+    A = P.filter(lambda i: i.decided)
+    return F.Spec(properties=[
+        ("SymCount", P.filter(lambda i: i.x == old(i.x)).size >= n // 2),
+        ("SymInitLe", P.forall(lambda i: P.exists(lambda j: init(j.x) <= i.x))),
+        ("SymPid", P.forall(lambda i: A.contains(i).implies(i.decision == i.x))),
+        ("SymNested", P.exists(lambda i: P.forall(lambda j: (j.x == i.x) | (init(j.x) > i.x)))),
+        ("SymCountEq", P.forall(lambda i: P.filter(lambda j: j.x == i.x).size == n)),
+        ("SymCoord", P.forall(lambda i: i.x >= F.coord.x) | (r > 100)),
+        ("SymPinGuard", V.exists(lambda v: (P.filter(lambda i: i.x == v).size > n // 2)
+                                 & P.forall(lambda i: i.decided.implies(i.decision == v)))),
+        ("SymMember", P.forall(lambda i: i.decided.implies(P.exists(lambda j: init(j.x) == i.decision)))),
+    ])
+
+
 # (id, algorithm, n, make_config kwargs, spec factory)
 CUSTOM = [
     ("fm-n12", psync.FloodMin(2), 12, dict(value_range=8, schedule=H(drop_log2=0, good_round=0.0, crash_fmax=3)),
@@ -144,4 +163,12 @@ CUSTOM = [
     ("otr-n16-order", psync.OTR(), 16, dict(value_range=3), order_shapes),
     ("lv-n8-order", psync.LastVoting(), 8, dict(value_range=3, schedule=H(drop_log2=1, good_round=0.0)),
      order_shapes),
+    # symmetric check points: n = 1 (every state), one initial value (from round 0), mixed
+    ("otr-n1-sym", psync.OTR(), 1, dict(value_range=3), symmetric_shapes),
+    ("otr-n16-v1-sym", psync.OTR(), 16, dict(value_range=1), symmetric_shapes),
+    ("otr-n16-sym", psync.OTR(), 16, dict(value_range=3), symmetric_shapes),
+    ("otr2-n100-v1-sym", psync.OTR2(), 100, dict(value_range=1), symmetric_shapes),
+    ("lv-n8-v1-sym", psync.LastVoting(), 8, dict(value_range=1), lv_custom),
+    ("fm-n8-sym", psync.FloodMin(2), 8, dict(value_range=2, schedule=H(drop_log2=0, good_round=0.0,
+                                                                        crash_fmax=3)), symmetric_shapes),
 ]
