@@ -109,6 +109,39 @@ bool tuple_fields(const Tree& T, int q, std::vector<std::pair<int, int>>& out) {
   return out.size() <= 4;
 }
 
+// Structural key of node e, bound variables numbered by binding depth from e (formula.py _skey):
+// two closed subformulas with equal keys are the same formula.
+std::string skey_rec(const Tree& T, int e, std::map<int, int>& env) {
+  const Node& n = T.nodes[e];
+  switch (n.k) {
+    case VAR: {
+      auto it = env.find(n.uid);
+      return it != env.end() ? "V" + std::to_string(it->second) : "free" + std::to_string(n.uid);
+    }
+    case LIT: return "L" + std::to_string(n.v);
+    case NV: return "N";
+    case RV: return "R";
+    case COORDV: return "K";
+    case FIELD: return "F(" + std::to_string(n.f) + "," + std::to_string(n.tag) + "," + skey_rec(T, n.a, env) + ")";
+    case UN: return "U(" + std::to_string(n.op) + "," + skey_rec(T, n.a, env) + ")";
+    case BIN:
+      return "B(" + std::to_string(n.op) + "," + skey_rec(T, n.a, env) + "," + skey_rec(T, n.b, env) + ")";
+    case QUANT:
+    case CONTAINS: {
+      const std::string pre = n.k == QUANT ? "Q(" + std::to_string(n.qk) + "," : "C(" + skey_rec(T, n.a, env) + ",";
+      const bool had = env.count(n.uid) > 0;
+      const int old = had ? env[n.uid] : 0;
+      const int level = (int)env.size();  // formula.py: {**env, uid: len(env)}
+      env[n.uid] = level;
+      const std::string body = skey_rec(T, n.k == QUANT ? n.a : n.b, env);
+      if (had) env[n.uid] = old;
+      else env.erase(n.uid);
+      return pre + body + ")";
+    }
+  }
+  throw SpecError("unsupported node");
+}
+
 // Does the body of process quantifier q read its variable only through current / old fields
 // (no init field, no use as a pid)? (formula.py _symmetric)
 bool symmetric(const Tree& T, int q) {
@@ -365,7 +398,14 @@ struct Gen {
   int max_vi = 0;
   std::map<int, std::map<std::pair<int, int>, std::string>> tuples;
   std::vector<int> init_sets;
-  std::map<int, std::string> cse;
+  std::map<std::string, std::string> cse;  // structural key of a closed subformula -> its hoisted value
+  std::map<int, std::string> skeys;         // skey memo per node
+  const std::string& skey(int e) {
+    auto it = skeys.find(e);
+    if (it != skeys.end()) return it->second;
+    std::map<int, int> env;
+    return skeys[e] = skey_rec(T, e, env);
+  }
   std::vector<std::pair<std::vector<std::pair<int, int>>, std::string>> tup_sets;
   std::set<std::vector<std::pair<int, int>>> tup_used;
   std::map<std::pair<int, int>, int> memo_slots;
@@ -388,7 +428,7 @@ struct Gen {
   }
 
   Code gen(int e, bool in_lane, int vi) {
-    auto c = cse.find(e);
+    auto c = cse.find(skey(e));
     if (c != cse.end()) return {c->second, false};  // a closed subformula computed once per check point
     const Node n = T.nodes[e];
     switch (n.k) {
@@ -744,24 +784,24 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
   std::vector<std::pair<std::string, int>> props;
   for (auto& p : P.props) props.emplace_back(p.first, rewrite_vint(T, p.second, memo));
   const int safety = P.sp < 0 ? -1 : rewrite_vint(T, P.sp, memo);
-  // common closed subformulas (the same node under several slots): hoisted, evaluated once per check point
+  // common closed subformulas (structurally equal, skey): hoisted, evaluated once per check point
   std::vector<int> roots = invs;
   for (auto& p : props)
     if (p.first != "Termination") roots.push_back(p.second);
   if (safety >= 0) roots.push_back(safety);
-  std::map<int, int> seen;
+  std::map<std::string, int> seen;
   std::vector<int> order;
   for (int rt : roots) {
     struct V {
-      static void visit(const Tree& T, int e, std::map<int, int>& seen, std::vector<int>& order) {
-        if (++seen[e] > 1) return;
+      static void visit(Gen& G, int e, std::map<std::string, int>& seen, std::vector<int>& order) {
+        if (++seen[G.skey(e)] > 1) return;
         std::vector<int> ch;
-        T.children(e, ch);
-        for (int c : ch) visit(T, c, seen, order);
+        G.T.children(e, ch);
+        for (int c : ch) visit(G, c, seen, order);
         order.push_back(e);  // post-order: inner subformulas first
       }
     };
-    V::visit(T, rt, seen, order);
+    V::visit(gen, rt, seen, order);
   }
   auto tup_decls = [&](const std::set<std::vector<std::pair<int, int>>>& used, const std::string& ind) {
     std::vector<std::string> out;
@@ -792,11 +832,11 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
     int slot = 0;
     for (int e : order) {
       const Kind kd = T.nodes[e].k;
-      if (seen[e] > 1 && (kd == QUANT || kd == CONTAINS) && free_of(T, e).empty()) {
+      if (seen[gen.skey(e)] > 1 && (kd == QUANT || kd == CONTAINS) && free_of(T, e).empty()) {
         const Code c = gen.gen(e, false, 0);
         const std::string name = pre + S((int)gen.cse.size());
         lines.push_back(ind + "const int32_t " + name + " = " + c.first + ";");
-        gen.cse[e] = name;
+        gen.cse[gen.skey(e)] = name;
       }
     }
     if (!invs.empty()) {
@@ -849,7 +889,8 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
   const bool has_term = G.has_term && !G.term.empty();
   const std::string term = G.term;
   std::vector<std::string> body, term_decls;
-  if (!gen.uft.empty()) {
+  // worth its test only with few fields to compare (formula.py SYMMETRIC_MAX_FIELDS)
+  if (!gen.uft.empty() && gen.uft.size() <= 6) {
     uint32_t cur = 0, old = 0;
     for (auto& ft : gen.uft) {
       if (ft.second == PSG_TAG_CUR) cur |= 1u << ft.first;

@@ -717,7 +717,8 @@ class _Gen:
         self.max_vi = 0
         self.tuples = {}      # var uid -> {(field, tag): C++ name} (serial quantifier over distinct states)
         self.init_sets = []   # fields f with an LDS membership set of init(f) (at most 2)
-        self.cse = {}         # id(closed subformula) -> C++ name of its hoisted value
+        self.cse = {}         # structural key of a closed subformula -> C++ name of its hoisted value
+        self.skeys = {}       # _skey memo
         self.tup_sets = {}    # field tuple of a distinct-state quantifier -> C++ name of its per-check-point TupU
         self.tup_used = set()  # field tuples used by the function being generated
         self.memo_slots = {}   # (init set, field) -> memo slot of member_init_own
@@ -728,8 +729,9 @@ class _Gen:
 
     def gen(self, e, in_lane, vi_depth):
         """(C++ expression, depends on the lane)."""
-        if id(e) in self.cse:
-            return self.cse[id(e)], False  # a closed subformula computed once per check point
+        k = _skey(e, self.skeys)
+        if k in self.cse:
+            return self.cse[k], False  # a closed subformula computed once per check point
         if isinstance(e, Lit):
             return _c_int(e.v), False
         if isinstance(e, NVal):
@@ -1015,6 +1017,43 @@ def _init_member(q):
     return None
 
 
+def _skey(e, memo):
+    """Structural key of e, bound variables numbered by binding depth from e: two closed
+    subformulas with equal keys are the same formula (common-subformula hoisting finds the
+    repeats of Formula text, where every occurrence is its own tree, as well as those of one
+    Python object)."""
+    got = memo.get(id(e))
+    if got is not None and got[0] is e:  # the key object is kept alive with its entry
+        return got[1]
+
+    def rec(x, env):
+        if isinstance(x, Var):
+            return ("V", env[x.uid]) if x.uid in env else ("free", x.uid)
+        if isinstance(x, Lit):
+            return ("L", x.v)
+        if isinstance(x, NVal):
+            return ("N",)
+        if isinstance(x, RVal):
+            return ("R",)
+        if isinstance(x, CoordVal):
+            return ("K",)
+        if isinstance(x, Field):
+            return ("F", x.f, x.tag, rec(x.proc, env))
+        if isinstance(x, Un):
+            return ("U", x.op, rec(x.x, env))
+        if isinstance(x, Bin):
+            return ("B", x.op, rec(x.x, env), rec(x.y, env))
+        if isinstance(x, Quant):
+            return ("Q", x.kind, rec(x.body, {**env, x.var.uid: len(env)}))
+        if isinstance(x, Contains):
+            return ("C", rec(x.e, env), rec(x.comp.body, {**env, x.comp.var.uid: len(env)}))
+        raise FormulaError(f"unsupported node {type(x).__name__}")
+
+    k = rec(e, {})
+    memo[id(e)] = (e, k)
+    return k
+
+
 def _symmetric(q):
     """Does the body of process quantifier q read its variable only through current / old
     fields (no init field, no use as a pid)?"""
@@ -1136,6 +1175,7 @@ SWAP_VINT = False
 # The symmetric-check-point lowering (spec::uniform); off only for A/B measurements (the C ABI's
 # generator, psg_spec_gen.cpp, always emits it).
 SYMMETRIC_LOWERING = True
+SYMMETRIC_MAX_FIELDS = 6  # (field, tag) pairs compared by spec::uniform; more: no symmetric lowering
 
 
 def _rewrite_vint(e, memo=None):
@@ -1216,16 +1256,17 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
     invs = [_rewrite_vint(inv if guard is None else (inv & guard), memo) for inv in spec.invariants]
     props = [(name, _rewrite_vint(f, memo)) for name, f in spec.properties]
     safety = None if spec.safety_predicate is None else _rewrite_vint(spec.safety_predicate, memo)
-    # common closed subformulas (the same Formula object used by several slots, e.g.
-    # OTR's keepInit in Invariant0 and Invariant1): hoisted, evaluated once per check point
+    # common closed subformulas (the same formula in several places, e.g. OTR's keepInit in
+    # Invariant0 and Invariant1; structurally equal, _skey): hoisted, evaluated once per check point
     roots = list(invs) + [f for name, f in props if name != "Termination"]
     if safety is not None:
         roots.append(safety)
     seen, order = {}, []
 
     def visit(e):
-        seen[id(e)] = seen.get(id(e), 0) + 1
-        if seen[id(e)] > 1:
+        k = _skey(e, gen.skeys)
+        seen[k] = seen.get(k, 0) + 1
+        if seen[k] > 1:
             return
         for c in e.children():
             visit(c)
@@ -1247,11 +1288,11 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
         lines = []
         slot = 0
         for e in order:
-            if seen[id(e)] > 1 and isinstance(e, (Quant, Contains)) and not _free_vars(e):
+            if seen[_skey(e, gen.skeys)] > 1 and isinstance(e, (Quant, Contains)) and not _free_vars(e):
                 c, _ = gen.gen(e, False, 0)
                 name = f"{pre}{len(gen.cse)}"
                 lines.append(f"{ind}const int32_t {name} = {c};")
-                gen.cse[id(e)] = name
+                gen.cse[_skey(e, gen.skeys)] = name
         iv = "uinv" if uni else "inv"
         if invs:
             for k, inv in enumerate(invs):
@@ -1286,7 +1327,10 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
     # the Spec reads): a second, scalar lowering, chosen per check point by spec::uniform
     ulines, uterm, uterm_decls, _ = block(True)
     gen.uni = False
-    if gen.uft and SYMMETRIC_LOWERING:
+    # worth its test only with few fields to compare: OTR's 5 (x, decided, decision; old decided,
+    # decision) are symmetric at 86 % of check points (fused OTR 13.4 -> 11.6 ms per 2.5e6
+    # instances), LastVoting's 9 almost never (22.9 -> 24.4 ms: the test is pure overhead)
+    if gen.uft and len(gen.uft) <= SYMMETRIC_MAX_FIELDS and SYMMETRIC_LOWERING:
         cur = sum(1 << f for f, t in gen.uft if t == TAG_CUR)
         old = sum(1 << f for f, t in gen.uft if t == TAG_OLD)
         lines = ([f"    if (spec::uniform<W, {cur}u, {old}u>(x)) {{"] + ulines + ["      return fb;", "    }"]

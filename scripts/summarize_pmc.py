@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-kernel PMC summary of a scripts/pmc_wide.sh run (several kernels, one process each pass).
 
-usage: summarize_pmc.py SRC DST --kernel 'NAME_SUBSTR=instances,rounds,n[,bytes_per_pr]' ...
+usage: summarize_pmc.py SRC DST --kernel 'NAME_SUBSTR[#k]=instances,rounds,n[,bytes_per_pr]' ...
+(#k: only the k-th dispatch of that kernel in each pass, 0-based, e.g. one row of a sweep)
 
 Writes DST/kernel_stats.csv (the --kernel-trace --stats summary) and DST/pmc_summary.json:
 per kernel, the per-launch counters, the instruction mix per instance-round, the issue
@@ -27,8 +28,12 @@ args = ap.parse_args()
 kernels = []
 for spec in args.kernel:
     name, nums = spec.rsplit("=", 1)
+    nth = None
+    if "#" in name:
+        name, k = name.rsplit("#", 1)
+        nth = int(k)
     v = [float(x) for x in nums.split(",")]
-    kernels.append((name, v[0], int(v[1]), int(v[2]), v[3] if len(v) > 3 else None))
+    kernels.append((name, v[0], int(v[1]), int(v[2]), v[3] if len(v) > 3 else None, nth))
 
 os.makedirs(args.dst, exist_ok=True)
 stats = os.path.join(args.src, "kt", "run_kernel_stats.csv")
@@ -37,7 +42,7 @@ if os.path.exists(stats):
     shutil.copy(stats, os.path.join(args.dst, "kernel_stats.csv"))
     for r in csv.DictReader(open(stats)):
         for k in kernels:
-            if k[0] in r["Name"]:
+            if k[0] in r["Name"] and k[5] is None:
                 avg_ns[k[0]] = float(r["AverageNs"])
 
 per = {k[0]: collections.defaultdict(list) for k in kernels}
@@ -55,12 +60,15 @@ for d in sorted(os.listdir(args.src)):
             by_dispatch[r["Dispatch_Id"]]["_dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             meta[k[0]] = {x: r[x] for x in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
                                             "Scratch_Size", "VGPR_Count", "SGPR_Count")}
-        for vals in by_dispatch.values():
+        disp = [by_dispatch[d] for d in sorted(by_dispatch, key=int)]
+        if k[5] is not None:
+            disp = disp[k[5]:k[5] + 1]
+        for vals in disp:
             for c, v in vals.items():
                 per[k[0]][c].append(v)
 
 out = {}
-for name, inst, R, n, bpr in kernels:
+for name, inst, R, n, bpr, _ in kernels:
     avg = {c: sum(v) / len(v) for c, v in per[name].items()}
     ns = avg_ns.get(name) or avg.get("_dur_ns")
     W = (n + 63) // 64
