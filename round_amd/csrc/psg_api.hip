@@ -877,6 +877,9 @@ int psg_run_batch_spec(psg_ctx* c, uint64_t inst_begin, uint64_t count, const ps
     unsigned long long host[NCOUNTERS_ALLOC];
     HIPCHK(c, hipMemcpyAsync(host, c->d_counters, sizeof(host), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    // a fused module compiled with -DPSG_PHASE_TIMERS=1 (formula.compile_native(defines=...)) run
+    // through a profiling build of the library
+    if (PSG_PHASE_TIMERS && std::getenv("PSG_PHASE_TIMERS")) print_timers(host);
     float ms = 0.f;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
     if (out) {

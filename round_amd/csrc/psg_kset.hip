@@ -151,8 +151,13 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
   sc.prep_good(0, P.lane, a.R);
   int32_t cr[W];
   pk_crash_rounds<W>(P, a, inst, cr);
-  int32_t x0[W], decision[W], dec_val[W], dec_round[W], halt_round[W];
-  uint32_t decider[W], decided[W], halted[W];
+  // A process decides and exits in the same round with decision = pick(t) (KSetAgreement.scala:
+  // 48-50): its decide value is `decision`, its decide round is its halt round, and decided =
+  // halted (halt_round >= 0) at every check point; decider is bit j of a flag word, with bit
+  // 8 + j the decision's "not an initial value" (its X0 probe, taken when it decides). Fewer
+  // live registers: 2 waves/SIMD with four 256-bit t masks per lane.
+  int32_t x0[W], decision[W], halt_round[W];
+  uint32_t fw = 0;
   Mask<W> t[W];
   int32_t xmin_l = INT32_MAX;
 #pragma unroll
@@ -165,9 +170,8 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
     // t = Map(id -> io.initialValue); decider = false (KSetAgreement.scala:27-31)
     t[j] = mzero<W>();
     if (P.val[j]) t[j].w[j] = 1ull << P.lane;
-    decision[j] = dec_val[j] = 0;
-    dec_round[j] = halt_round[j] = -1;
-    decider[j] = decided[j] = halted[j] = 0;
+    decision[j] = 0;
+    halt_round[j] = -1;
   }
   X0Set<W> X0;
   pk_x0_build<W>(P, X0, x0lds, x0);  // ends with an LDS fence: x0s visible too
@@ -178,10 +182,15 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
   const Mask<W> Emin = P.ballot(emin);
   Checks ck;
   ck.reset();
-  uint32_t notinit[W];  // X0 probe of each slot's decision, taken when it decides (pk_kagree_check_m)
+  auto check = [&](int c) {
+    uint32_t decided[W], notinit[W];
 #pragma unroll
-  for (int j = 0; j < W; ++j) notinit[j] = 0;
-  auto check = [&](int c) { pk_kagree_check_m<W>(P, ck, c, kk, decided, decision, cr, notinit); };
+    for (int j = 0; j < W; ++j) {
+      decided[j] = halt_round[j] >= 0 ? 1u : 0u;
+      notinit[j] = (fw >> (8 + j)) & 1u;
+    }
+    pk_kagree_check_m<W>(P, ck, c, kk, decided, decision, cr, notinit);
+  };
   check(0);
   pt.mark(0);
   Mask<W> act;
@@ -206,7 +215,10 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
           CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
         }
       }
-      const Mask<W> Dm = mand(P.ballot(decider), act);  // senders' decider flags (pre-state)
+      uint32_t dw[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) dw[j] = (fw >> j) & 1u;
+      const Mask<W> Dm = mand(P.ballot(dw), act);  // senders' decider flags (pre-state)
 #pragma unroll
       for (int j = 0; j < W; ++j)
 #pragma unroll
@@ -300,8 +312,10 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
 #pragma unroll
       for (int j = 0; j < W; ++j) {
         uint32_t becomeDec = 0;
+        const bool halted = halt_round[j] >= 0;  // before this round (set below when it decides)
+        const uint32_t decider = (fw >> j) & 1u;
         const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
-        const uint32_t live = P.val[j] & (1u - halted[j]) & (1u - decider[j]);
+        const uint32_t live = P.val[j] & (halted ? 0u : 1u) & (1u - decider);
         const uint32_t hc = many(mand(M, Dm)) ? 1u : 0u;
         const uint32_t adopt = live & hc, mergep = live & (1u - hc);
         Mask<W> tnew = t[j];
@@ -360,26 +374,22 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
           tnew = load_t<W, 64 * W>(L.ts, kset_find<W, 64 * W>(a, L.ts, M, mand(M, Dm), cols ? L.hol : nullptr, ncols));
           becomeDec = 1;
         }
-        if (!halted[j] && decider[j]) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:48-50)
+        if (!halted && decider) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:48-50)
           const int32_t v = kset_pick<W>(t[j], L.x0s, Emin, xmin);
-          dec_val[j] = v;
-          dec_round[j] = k;
-          decided[j] = 1;
           decision[j] = v;
-          notinit[j] = 1u - X0.contains01(v);
+          fw |= (1u - X0.contains01(v)) << (8 + j);
           halt_round[j] = k;
         }
-        if (!halted[j]) {  // the post-round state of slot j (its pre-round t is in the staging)
+        if (!halted) {  // the post-round state of slot j (its pre-round t is in the staging)
           t[j] = tnew;
-          decider[j] |= becomeDec;
+          fw |= becomeDec << j;
         }
       }
       lds_sync<1>();  // all reads of ts done before the next round restages it
       uint32_t al[W];
 #pragma unroll
       for (int j = 0; j < W; ++j) {
-        if (halt_round[j] == k) halted[j] = 1;
-        al[j] = P.val[j] & (1u - halted[j]);
+        al[j] = P.val[j] & (halt_round[j] >= 0 ? 0u : 1u);
       }
       act = P.ballot(al);
       pt.mark(2);
@@ -390,13 +400,13 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
   int32_t mainx[W];
 #pragma unroll
   for (int j = 0; j < W; ++j) mainx[j] = P.val[j] ? kset_pick<W>(t[j], L.x0s, Emin, xmin) : 0;
-  pk_finish<W>(P, a, i, ck, 2, dec_val, dec_round, halt_round, mainx, bc);
+  pk_finish<W>(P, a, i, ck, 2, decision, halt_round, halt_round, mainx, bc);
   lds_sync<1>();  // x0s / ts reads done before the next instance restages them
   pt.mark(3);
 }
 
 #ifndef PSG_KSET_PK_WPE
-#define PSG_KSET_PK_WPE 2  // W = 4 packs four 256-bit t masks (and their next values) per lane
+#define PSG_KSET_PK_WPE 3  // W = 4: four 256-bit t masks per lane; 2 -> 3 after the per-slot state diet: C4 f=1 2.80 -> 2.18 ms
 #endif
 template <int W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_KSET_PK_WPE))) kset_packed_kernel(KArgs a) {

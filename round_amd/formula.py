@@ -1414,7 +1414,7 @@ def _fused_source(alg: int, waves: Sequence[int]) -> str:
 
 
 def compile_native(spec: Spec, alg: Optional[int] = None, cache_dir: str = None, hipcc: str = None,
-                   fused: bool = False, n: Optional[int] = None) -> Program:
+                   fused: bool = False, n: Optional[int] = None, defines: Sequence[str] = ()) -> Program:
     """Lower `spec` to native gfx950 code (hipcc --genco, cached by source hash) and
     return a Program whose module_path psg_run_batch_spec launches instead of the
     bytecode interpreter.
@@ -1422,7 +1422,9 @@ def compile_native(spec: Spec, alg: Optional[int] = None, cache_dir: str = None,
     fused=True also instantiates the algorithm's round kernel with the Spec as its
     check hook (spec::SpecHook): psg_run_batch_spec then runs ONE launch that
     executes the rounds and evaluates the Spec from registers, with no state trace.
-    `n` (optional) limits the instantiations to that group size's wave count."""
+    `n` (optional) limits the instantiations to that group size's wave count. `defines`: extra
+    preprocessor definitions (e.g. "PSG_PHASE_TIMERS=1" for a profiling module; part of the
+    cache key)."""
     import hashlib
     import os
     import subprocess
@@ -1437,14 +1439,16 @@ def compile_native(spec: Spec, alg: Optional[int] = None, cache_dir: str = None,
     cache_dir = cache_dir or CACHE_DIR
     os.makedirs(cache_dir, exist_ok=True)
     hdrs = "".join(open(os.path.join(_CSRC, h)).read() for h in hdr_names)
-    key = hashlib.sha256((src + hdrs + open(os.path.join(_INCLUDE, "psg.h")).read()).encode()).hexdigest()[:24]
+    dflags = [f"-D{d}" for d in defines]
+    key_src = src + hdrs + open(os.path.join(_INCLUDE, "psg.h")).read() + ("".join(dflags) if dflags else "")
+    key = hashlib.sha256(key_src.encode()).hexdigest()[:24]
     out = os.path.join(cache_dir, f"spec_{key}.co")
     if not os.path.exists(out):
         path = os.path.join(cache_dir, f"spec_{key}.hip")
         with open(path, "w") as f:
             f.write(src)
         cmd = [hipcc or os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), "--genco", "--offload-arch=gfx950", "-O3",
-               "-std=c++17", "-I", _CSRC, "-I", _INCLUDE, path, "-o", out + ".tmp"]
+               "-std=c++17", "-I", _CSRC, "-I", _INCLUDE, *dflags, path, "-o", out + ".tmp"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise FormulaError("native spec compile failed:\n" + r.stderr[-4000:])

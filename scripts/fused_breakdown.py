@@ -48,13 +48,19 @@ def main():
     ap.add_argument("--instances", type=int, default=2_500_000)
     ap.add_argument("--alg", default="otr")
     ap.add_argument("--nosym", action="store_true")
+    ap.add_argument("--timers", action="store_true",
+                    help="profiling modules (-DPSG_PHASE_TIMERS=1) of the full Spec and the round kernel alone; "
+                         "run with PSG_LIB=round_amd/libpsg_timers.so PSG_PHASE_TIMERS=1")
     args = ap.parse_args()
     F.SYMMETRIC_LOWERING = not args.nosym
     if args.alg == "otr":
         alg, aid, kw, variants = psync.OTR(), abi.PSG_ALG_OTR, dict(value_range=64), otr_variants()
     else:
         alg, aid, kw, variants = psync.LastVoting(), abi.PSG_ALG_LAST_VOTING, {}, lv_variants()
-    progs = {k: formula.compile_native(s, aid, fused=True, n=64) for k, s in variants.items()}
+    if args.timers:
+        variants = {k: v for k, v in variants.items() if k in ("full", "rounds_only")}
+    defs = ("PSG_PHASE_TIMERS=1",) if args.timers else ()
+    progs = {k: formula.compile_native(s, aid, fused=True, n=64, defines=defs) for k, s in variants.items()}
     if args.compile_only:
         print("compiled", len(progs))
         return

@@ -1,4 +1,5 @@
-"""A/B probe of the headline launch (OTR n=64, 1e7 instances, R=20, V=64 and V=2; arg lv: C3 LastVoting):
+"""A/B probe of the headline launch (OTR n=64, 1e7 instances, R=20, V=64 and V=2; arg lv: C3 LastVoting;
+kset: the C4 KSet rows at f = 1, 16, 64):
 min kernel ms over 5 launches for the library PSG_LIB points at (default: in-tree)."""
 import os
 import sys
@@ -9,10 +10,15 @@ from round_amd import lib, psync  # noqa: E402
 which = sys.argv[1] if len(sys.argv) > 1 else "otr"
 if which == "otr":
     runs = [(psync.OTR(), 10_000_000, dict(value_range=V), f"V={V}") for V in (64, 2)]
+elif which == "kset":  # C4 KSet rows (bench_configs.py): n=256, k=2, 2e5 instances, R=16, crash-stop f
+    runs = [(psync.KSetAgreement(2), 200_000, dict(schedule=psync.HOSchedule(drop_log2=0, good_round=0.0,
+                                                                              crash_fmax=f)), f"KSet f={f}")
+            for f in (1, 16, 64)]
 else:  # BASELINE C3 shard: LastVoting n=64, 1.25e7 instances, crash-stop
     runs = [(psync.LastVoting(), 12_500_000, {}, "LV C3")]
 for alg, I, kw, label in runs:
-    with psync.GpuRound(alg, 64, 20, seed=2, batch_capacity=I, **kw) as g:
+    n, R = (256, 16) if which == "kset" else (64, 20)
+    with psync.GpuRound(alg, n, R, seed=2, batch_capacity=I, **kw) as g:
         g.load_inputs(0, I)
         g.run(0, I)
         ks = [g.run(0, I).summary.kernel_ns / 1e6 for _ in range(5)]
