@@ -169,19 +169,18 @@ PSG_DEV void floodmin_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_
   sc.setup(a, inst, P.lane, false);  // uniform parts; crash rounds per slot below
   int32_t cr[W];
   pk_crash_rounds<W>(P, a, inst, cr);
-  int32_t x[W], decision[W], dec_val[W], dec_round[W], halt_round[W];
-  uint32_t dec01[W], halt01[W];
+  // Every process decides x and exits in the same round (decideNow is uniform,
+  // FloodMin.scala:27-31): the decide / halt round dk is one uniform value (-1 until then), a
+  // decision is the process's x, and bit j of nib is "slot j's decision is not an initial
+  // value" (its X0 probe, taken when it decides: the decision never changes afterwards).
+  int32_t x[W];
+  int dk = -1;
+  uint32_t nib = 0;
 #pragma unroll
   for (int j = 0; j < W; ++j) {
     x[j] = 0;
     if (P.val[j])
       x[j] = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + P.pid(j)] : sc.init_value(P.pid(j), PSG_ALG_FLOODMIN);
-    decision[j] = 0;
-    dec_val[j] = 0;
-    dec_round[j] = -1;
-    halt_round[j] = -1;
-    dec01[j] = 0;
-    halt01[j] = 0;
   }
   X0Set<W> X0;
   pk_x0_build<W>(P, X0, x0lds, x);
@@ -193,18 +192,19 @@ PSG_DEV void floodmin_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_
   auto check = [&](int c) {
     uint32_t anyY = 0, anyBad = 0, undec = 0, alive[W];
     int32_t mu = INT32_MAX, dmn = INT32_MAX, dmx = INT32_MIN;
+    const uint32_t dec01 = dk >= 0 ? 1u : 0u;  // every process decided (and halted) in round dk
 #pragma unroll
     for (int j = 0; j < W; ++j) {
       const uint32_t crashed = cr[j] >= 0 ? 1u : 0u;
-      alive[j] = P.val[j] & (1u - halt01[j]);
+      alive[j] = P.val[j] & (1u - dec01);
       const uint32_t inU = alive[j] & (1u - (crashed & (cr[j] <= c ? 1u : 0u)));  // not crashed before or in round c
-      const uint32_t dc = P.val[j] & dec01[j] & (1u - crashed);
+      const uint32_t dc = P.val[j] & dec01 & (1u - crashed);
       mu = inU ? min(mu, x[j]) : mu;
-      dmn = dc ? min(dmn, decision[j]) : dmn;
-      dmx = dc ? max(dmx, decision[j]) : dmx;
+      dmn = dc ? min(dmn, x[j]) : dmn;  // decision = x
+      dmx = dc ? max(dmx, x[j]) : dmx;
       anyY |= dc;
-      anyBad |= P.val[j] & dec01[j] & (1u - X0.contains01(decision[j]));
-      undec |= P.val[j] & (1u - dec01[j]);
+      anyBad |= P.val[j] & dec01 & ((nib >> j) & 1u);
+      undec |= P.val[j] & (1u - dec01);
     }
     act = P.ballot(alive);
     mU = Grp<1>::dpp_reduce32<false>(mu);
@@ -251,23 +251,23 @@ PSG_DEV void floodmin_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_
         }
       }
       const bool decideNow = a.variant == 1 ? (k >= f - 1) : (k > f);  // FloodMin.scala:27 (variant 1: mutation)
+      // (the round runs only while every process is alive: they all decide together)
 #pragma unroll
       for (int j = 0; j < W; ++j) {
-        if (halt01[j]) continue;
         x[j] = nx[j];
-        if (decideNow) {
-          dec_val[j] = x[j];
-          dec_round[j] = k;
-          dec01[j] = 1;
-          decision[j] = x[j];
-          halt_round[j] = k;
-          halt01[j] = 1;
-        }
+        if (decideNow) nib |= (1u - X0.contains01(x[j])) << j;
       }
+      if (decideNow) dk = k;
     }
     check(k + 1);
   }
-  pk_finish<W>(P, a, i, ck, 2, dec_val, dec_round, halt_round, x, bc);
+  int32_t dv[W], dr[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    dv[j] = dk >= 0 ? x[j] : 0;
+    dr[j] = dk;
+  }
+  pk_finish<W>(P, a, i, ck, 2, dv, dr, dr, x, bc);
 }
 
 template <int W>
