@@ -41,7 +41,8 @@ PSG_DEV void kset_es_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t
   // slot; canDecide and halted are bits j / 8 + j of one flag word.
   int32_t est[W], decision[W];
   uint32_t nbh[W];  // lastNb (bits 0..15) | halt round + 1 (bits 16..31: 0 = not halted)
-  uint32_t fl = 0;  // bit j: canDecide of slot j; bit 8 + j: slot j halted (or not a process)
+  uint32_t fl = 0;  // bit j: canDecide of slot j; bit 8 + j: slot j halted (or not a process);
+                    // bit 16 + j: slot j's decision is not an initial value (probed when it decides)
 #pragma unroll
   for (int j = 0; j < W; ++j) {
     est[j] = 0;
@@ -56,10 +57,13 @@ PSG_DEV void kset_es_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t
   Checks ck;
   ck.reset();
   auto check = [&](int c) {
-    uint32_t decided[W];
+    uint32_t decided[W], notinit[W];
 #pragma unroll
-    for (int j = 0; j < W; ++j) decided[j] = P.val[j] & ((fl >> (8 + j)) & 1u);
-    pk_kagree_check<W>(P, ck, c, kk, decided, decision, cr, X0);
+    for (int j = 0; j < W; ++j) {
+      decided[j] = P.val[j] & ((fl >> (8 + j)) & 1u);
+      notinit[j] = (fl >> (16 + j)) & 1u;
+    }
+    pk_kagree_check_m<W>(P, ck, c, kk, decided, decision, cr, notinit);
   };
   check(0);
   for (int k = 0; k < a.R; ++k) {
@@ -161,7 +165,7 @@ PSG_DEV void kset_es_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t
         if ((dnow >> j) & 1u) {  // callback.decide(est); exitAtEndOfRound (KSetEarlyStopping.scala:32-34)
           decision[j] = est[j];
           nbh[j] = (nbh[j] & 0xFFFFu) | ((uint32_t)(k + 1) << 16);
-          fl |= 1u << (8 + j);
+          fl |= (1u << (8 + j)) | ((1u - X0.contains01(est[j])) << (16 + j));
         } else if (!((fl >> (8 + j)) & 1u)) {
           est[j] = nest[j];
         }

@@ -115,7 +115,7 @@ PSG_DEV void pk_x0_build(const Pk<W>& P, X0Set<W>& X, int32_t* lds, const int32_
 // crashed deciders number <= k; slot 1 — every decision is an initial value; termination
 // when every process decided. notinit: per slot, "decided and its decision is not an initial
 // value" — the X0 probe of a decision, taken by the caller when the decision is made (a
-// decision never changes afterwards), or here (pk_kagree_check).
+// decision never changes afterwards).
 template <int W>
 PSG_DEV void pk_kagree_check_m(const Pk<W>& P, Checks& ck, int c, int kk, const uint32_t (&decided)[W],
                                const int32_t (&decision)[W], const int32_t (&cr)[W], const uint32_t (&notinit)[W]) {
@@ -137,15 +137,6 @@ PSG_DEV void pk_kagree_check_m(const Pk<W>& P, Checks& ck, int c, int kk, const 
     ++distinct;
   }
   ck.record(fbit(distinct <= kk, 0) | fbit(!pk_any(bad), 1), !pk_any(undec), c, P.lane);
-}
-
-template <int W>
-PSG_DEV void pk_kagree_check(const Pk<W>& P, Checks& ck, int c, int kk, const uint32_t (&decided)[W],
-                             const int32_t (&decision)[W], const int32_t (&cr)[W], const X0Set<W>& X0) {
-  uint32_t notinit[W];
-#pragma unroll
-  for (int j = 0; j < W; ++j) notinit[j] = 1u - X0.contains01(decision[j]);
-  pk_kagree_check_m<W>(P, ck, c, kk, decided, decision, cr, notinit);
 }
 
 // Per-instance epilogue of a packed instance (finish_instance for W slots per lane):

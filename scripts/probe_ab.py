@@ -16,12 +16,15 @@ elif which == "kset":  # C4 KSet rows (bench_configs.py): n=256, k=2, 2e5 instan
             for f in (1, 16, 64)]
 elif which == "fm":  # C4 FloodMin rows (bench_configs.py): n=256, 1e6 instances, default schedule, R = f + 2
     runs = [(psync.FloodMin(f), 1_000_000, {}, f"FloodMin f={f}") for f in (0, 8, 64)]
+elif which == "kses":  # W2 KSetEarlyStopping: n=256, t=64, k=2, 1e6 instances, default rounds / schedule
+    runs = [(psync.KSetEarlyStopping(64, 2), 1_000_000, {}, "KSetES W2")]
 elif which == "benor":  # C5: BenOr n=128, 1e6 instances, R=64
     runs = [(psync.BenOr(), 1_000_000, {}, "BenOr C5")]
 else:  # BASELINE C3 shard: LastVoting n=64, 1.25e7 instances, crash-stop
     runs = [(psync.LastVoting(), 12_500_000, {}, "LV C3")]
 for alg, I, kw, label in runs:
-    n, R = {"kset": (256, 16), "fm": (256, None), "benor": (128, 64)}.get(which, (64, 20))  # None: R = f + 2
+    n, R = {"kset": (256, 16), "fm": (256, None), "kses": (256, None), "benor": (128, 64)}.get(
+        which, (64, 20))  # None: the algorithm's default rounds
     with psync.GpuRound(alg, n, R, seed=2, batch_capacity=I, **kw) as g:
         g.load_inputs(0, I)
         g.run(0, I)
