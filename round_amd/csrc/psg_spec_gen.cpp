@@ -19,6 +19,7 @@
 #include <cstring>
 #include <dlfcn.h>
 #include <fstream>
+#include <functional>
 #include <mutex>
 #include <set>
 #include <sstream>
@@ -159,6 +160,25 @@ bool symmetric(const Tree& T, int q) {
     }
   }
   return nvar == nfield;
+}
+
+// Conjuncts A of forall(j => A && .. ==> B) / exists, count(j => A && .. && B) that read only j
+// (formula.py _tuple_guard): the processes where one fails contribute nothing
+std::vector<int> tuple_guard(const Tree& T, int q) {
+  const Node& Q = T.nodes[q];
+  std::vector<int> cs, out;
+  if (Q.qk == QFORALL) {
+    const Node& b = T.nodes[Q.a];
+    if (!(b.k == BIN && b.op == PSG_OP_IMPL)) return out;
+    conjuncts(T, b.a, cs);
+  } else {
+    conjuncts(T, Q.a, cs);
+  }
+  for (int c : cs) {
+    const std::set<int> fv = free_of(T, c);
+    if (fv.size() == 1 && fv.count(Q.uid) && !expensive(T, c)) out.push_back(c);
+  }
+  return out;
 }
 
 // breakpoint offsets (bit d+1: b = e + d) of an atom `t OP e`, t the V.exists variable
@@ -406,8 +426,10 @@ struct Gen {
     std::map<int, int> env;
     return skeys[e] = skey_rec(T, e, env);
   }
-  std::vector<std::pair<std::vector<std::pair<int, int>>, std::string>> tup_sets;
-  std::set<std::vector<std::pair<int, int>>> tup_used;
+  // (field tuple, guard code or "") -> TupU / TupG name (formula.py tup_sets)
+  using TupKey = std::pair<std::vector<std::pair<int, int>>, std::string>;
+  std::vector<std::pair<TupKey, std::string>> tup_sets;
+  std::set<TupKey> tup_used;
   std::map<std::pair<int, int>, int> memo_slots;
   bool uni = false;                          // lowering for symmetric check points (spec::uniform)
   std::set<int> pvars;                       // variables bound to a process (a pid in [0, n))
@@ -571,6 +593,16 @@ struct Gen {
       if (tuple_fields(T, q, flds)) {
         // the body reads j only through fields: visit each distinct field tuple once
         // (count: weighted by how many processes hold it)
+        const std::vector<int> guard = flds.empty() ? std::vector<int>{} : tuple_guard(T, q);
+        std::string gcode;
+        if (!guard.empty()) {
+          // A(j) of forall(j => A(j) ==> B) / exists, count(j => A(j) && B): only the processes
+          // where it holds are visited; evaluated per lane (j = the lane's own process)
+          names[Q.uid] = Name{v, true, true};
+          for (size_t i = 0; i < guard.size(); ++i)
+            gcode += (i ? " & " : "") + std::string("(int32_t)((") + gen(guard[i], true, vi).first + ") != 0)";
+          names.erase(Q.uid);
+        }
         std::map<std::pair<int, int>, std::string> nm;
         for (size_t i = 0; i < flds.size(); ++i) nm[flds[i]] = v + "_" + S((int)i);
         tuples[Q.uid] = nm;
@@ -587,15 +619,16 @@ struct Gen {
         }
         if (flds.empty())
           return {"spec::quant_tup<W, " + S(mode) + ">(x, " + lam(params, body.first) + ")", body.second};
-        // per check point: are those fields the same for every process (one tuple)?
-        auto ts = std::find_if(tup_sets.begin(), tup_sets.end(), [&](const auto& p) { return p.first == flds; });
+        // per check point: are those fields the same for every (guarded) process (one tuple)?
+        const TupKey key{flds, gcode};
+        auto ts = std::find_if(tup_sets.begin(), tup_sets.end(), [&](const auto& p) { return p.first == key; });
         if (ts == tup_sets.end()) {
-          tup_sets.emplace_back(flds, "tu" + S((int)tup_sets.size()));
+          tup_sets.emplace_back(key, "tu" + S((int)tup_sets.size()));
           ts = tup_sets.end() - 1;
         }
-        tup_used.insert(flds);
-        return {"spec::quant_tup_c<W, " + S(mode) + ">(x, " + ts->second + ", " + lam(params, body.first) + ", " + fl +
-                    ")",
+        tup_used.insert(key);
+        return {std::string("spec::") + (gcode.empty() ? "quant_tup_c" : "quant_tup_gc") + "<W, " + S(mode) + ">(x, " +
+                    ts->second + ", " + lam(params, body.first) + ", " + fl + ")",
                 body.second};
       }
       names[Q.uid] = Name{v, false, false};
@@ -803,14 +836,19 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
     };
     V::visit(gen, rt, seen, order);
   }
-  auto tup_decls = [&](const std::set<std::vector<std::pair<int, int>>>& used, const std::string& ind) {
+  auto tup_decls = [&](const std::set<Gen::TupKey>& used, const std::string& ind) {
     std::vector<std::string> out;
     for (auto& ts : gen.tup_sets) {
       if (!used.count(ts.first)) continue;
+      const auto& flds = ts.first.first;
       std::string fl;
-      for (size_t i = 0; i < ts.first.size(); ++i)
-        fl += (i ? ", " : "") + std::string("spec::Fld<") + S(ts.first[i].first) + ", " + S(ts.first[i].second) + ">{}";
-      out.push_back(ind + "const auto " + ts.second + " = spec::tup_uniform<W>(x, " + fl + ");");
+      for (size_t i = 0; i < flds.size(); ++i)
+        fl += (i ? ", " : "") + std::string("spec::Fld<") + S(flds[i].first) + ", " + S(flds[i].second) + ">{}";
+      if (ts.first.second.empty())
+        out.push_back(ind + "const auto " + ts.second + " = spec::tup_uniform<W>(x, " + fl + ");");
+      else
+        out.push_back(ind + "const auto " + ts.second + " = spec::tup_uniform_g<W>(x, " + ts.first.second + ", " + fl +
+                      ");");
     }
     return out;
   };
@@ -829,21 +867,28 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
     const std::string ind = uni ? "      " : "    ", pre = uni ? "ucse" : "cse", iv = uni ? "uinv" : "inv";
     Block B;
     std::vector<std::string> lines;
+    // a distinct-state tuple test is declared just before the first line that uses it
+    auto add = [&](int e, const std::function<std::string(const std::string&)>& fmt) {
+      const std::set<Gen::TupKey> before = gen.tup_used;
+      const Code c = gen.gen(e, false, 0);
+      std::set<Gen::TupKey> fresh;
+      for (auto& k : gen.tup_used)
+        if (!before.count(k)) fresh.insert(k);
+      for (auto& d : tup_decls(fresh, ind)) lines.push_back(d);
+      lines.push_back(fmt(c.first));
+    };
     int slot = 0;
     for (int e : order) {
       const Kind kd = T.nodes[e].k;
       if (seen[gen.skey(e)] > 1 && (kd == QUANT || kd == CONTAINS) && free_of(T, e).empty()) {
-        const Code c = gen.gen(e, false, 0);
         const std::string name = pre + S((int)gen.cse.size());
-        lines.push_back(ind + "const int32_t " + name + " = " + c.first + ";");
+        add(e, [&](const std::string& c) { return ind + "const int32_t " + name + " = " + c + ";"; });
         gen.cse[gen.skey(e)] = name;
       }
     }
     if (!invs.empty()) {
-      for (size_t k = 0; k < invs.size(); ++k) {
-        const Code c = gen.gen(invs[k], false, 0);
-        lines.push_back(ind + "const int32_t " + iv + S((int)k) + " = " + c.first + ";");
-      }
+      for (size_t k = 0; k < invs.size(); ++k)
+        add(invs[k], [&](const std::string& c) { return ind + "const int32_t " + iv + S((int)k) + " = " + c + ";"; });
       std::string any;
       for (size_t k = 0; k < invs.size(); ++k) any += (k ? " | " : "") + std::string("(") + iv + S((int)k) + " != 0)";
       lines.push_back(ind + "if (!(" + any + ")) fb |= 1u << " + S(slot) + ";");
@@ -853,7 +898,7 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
         ++slot;
       }
     }
-    std::set<std::vector<std::pair<int, int>>> term_tups;
+    std::set<Gen::TupKey> term_tups;
     for (auto& p : props) {
       if (p.first == "Termination") {
         auto saved = gen.tup_used;
@@ -864,18 +909,19 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
         gen.tup_used = saved;
         continue;
       }
-      const Code c = gen.gen(p.second, false, 0);
-      lines.push_back(ind + "if ((" + c.first + ") == 0) fb |= 1u << " + S(slot) + ";  // " + p.first);
+      add(p.second, [&](const std::string& c) {
+        return ind + "if ((" + c + ") == 0) fb |= 1u << " + S(slot) + ";  // " + p.first;
+      });
       ++slot;
     }
     if (safety >= 0) {
-      const Code c = gen.gen(safety, false, 0);
-      lines.push_back(ind + "if ((" + c.first + ") == 0) fb |= 1u << " + S(slot) + ";  // SafetyPredicate");
+      add(safety, [&](const std::string& c) {
+        return ind + "if ((" + c + ") == 0) fb |= 1u << " + S(slot) + ";  // SafetyPredicate";
+      });
       ++slot;
     }
     if (slot != (int)prog.entry.size()) throw SpecError("native lowering: slot count mismatch");
-    B.lines = tup_decls(gen.tup_used, ind);
-    B.lines.insert(B.lines.end(), lines.begin(), lines.end());
+    B.lines = lines;
     B.term_decls = tup_decls(term_tups, ind);
     B.slot = slot;
     return B;

@@ -241,6 +241,78 @@ PSG_DEV int32_t quant_tup_c(Ctx<W>& x, const TupU<NF>& tu, Fn fn, Fs... fs) {
   return quant_tup<W, MODE>(x, fn, fs...);
 }
 
+// Guarded distinct-state quantifiers: P.forall(j => A(j) ==> B), P.exists(j => A(j) && B) and
+// the count of A(j) && B visit only the processes where A holds (A reads only j's fields; the
+// others contribute nothing), so their tuples are those of the guard set G — one tuple when
+// every guarded process agrees (LastVoting's Agreement over the deciders while crashed
+// processes never decide). tup_uniform_g: G = ballot(guard), the tuple of G's first process
+// and whether every process of G holds it; G empty: the quantifier's identity.
+template <int W, int NF>
+struct TupG {
+  bool uni, empty;
+  Mask<W> G;
+  int32_t v[NF];
+};
+
+template <int W, class... Fs>
+PSG_DEV TupG<W, (int)sizeof...(Fs)> tup_uniform_g(Ctx<W>& x, int32_t guard, Fs...) {
+  TupG<W, (int)sizeof...(Fs)> t;
+  t.G = x.g.ballot(guard != 0);
+  t.empty = !many(t.G);
+  const int q0 = t.empty ? 0 : mfirst(t.G);
+  uint32_t diff = 0;
+  int k = 0;
+  auto one = [&](auto fld) {
+    using FL = decltype(fld);
+    const int32_t mine = x.own(FL::tag, FL::f);
+    t.v[k] = x.g.bcast(mine, x.stage(FL::tag, FL::f), q0);
+    diff |= ne01(mine, t.v[k]);
+    ++k;
+  };
+  (one(Fs{}), ...);
+  t.uni = !x.g.any(guard != 0 && diff != 0u);
+  return t;
+}
+
+template <int W, int MODE, int NF, class Fn, class... Fs>
+PSG_DEV int32_t quant_tup_gc(Ctx<W>& x, const TupG<W, NF>& tu, Fn fn, Fs...) {
+  if (tu.empty) return MODE == 0 ? 1 : 0;
+  if (tu.uni) {
+    int32_t b;
+    if constexpr (NF == 1) b = fn(tu.v[0]);
+    else if constexpr (NF == 2) b = fn(tu.v[0], tu.v[1]);
+    else if constexpr (NF == 3) b = fn(tu.v[0], tu.v[1], tu.v[2]);
+    else b = fn(tu.v[0], tu.v[1], tu.v[2], tu.v[3]);
+    if constexpr (MODE == 2) return b != 0 ? mpopc(tu.G) : 0;
+    else return b != 0 ? 1 : 0;
+  }
+  int32_t acc = MODE == 0 ? 1 : 0;
+  Mask<W> rem = tu.G;
+  while (many(rem)) {
+    const int q = mfirst(rem);
+    Mask<W> E = rem;
+    auto val = [&](auto fld) -> int32_t {
+      using FL = decltype(fld);
+      const int32_t mine = x.own(FL::tag, FL::f);
+      const int32_t v = x.g.bcast(mine, x.stage(FL::tag, FL::f), q);
+      E = mand(E, x.g.ballot(mine == v));
+      return v;
+    };
+    const int32_t b = fn(val(Fs{})...);
+    rem = mandn(rem, E);
+    if constexpr (MODE == 0) {
+      acc = (acc != 0 && b != 0) ? 1 : 0;
+      if (!x.g.any(acc != 0)) break;
+    } else if constexpr (MODE == 1) {
+      acc = (acc != 0 || b != 0) ? 1 : 0;
+      if (!x.g.any(acc == 0)) break;
+    } else {
+      acc += b != 0 ? mpopc(E) : 0;
+    }
+  }
+  return acc;
+}
+
 // P.exists(j => init(j.f) == t): membership of t in the instance's set of initial
 // values of f — an LDS hash set built once per instance (X0Set), as the
 // hand-lowered checks do, instead of a loop over the processes.

@@ -837,6 +837,14 @@ class _Gen:
             if flds is not None:
                 # the body reads j only through fields: visit each distinct field tuple once
                 # (count: weighted by how many processes hold it)
+                guard = _tuple_guard(q) if flds else []
+                gcode = None
+                if guard:
+                    # A(j) of forall(j => A(j) ==> B) / exists, count(j => A(j) && B): only the
+                    # processes where it holds are visited; evaluated per lane (j = the lane's own)
+                    self.names[q.var.uid] = (v, True, True)
+                    gcode = " & ".join(f"(int32_t)(({self.gen(c, True, vi_depth)[0]}) != 0)" for c in guard)
+                    del self.names[q.var.uid]
                 names = {ft: f"{v}_{k}" for k, ft in enumerate(flds)}
                 self.tuples[q.var.uid] = names
                 for f, tag in flds:
@@ -850,12 +858,13 @@ class _Gen:
                 fl = ", ".join(f"spec::Fld<{f}, {tag}>{{}}" for f, tag in flds)
                 if not flds:
                     return (f"spec::quant_tup<W, {mode}>(x, [&]({params}) -> int32_t {{ return {body}; }})"), lane
-                # per check point: are those fields the same for every process (one tuple)?
-                key = tuple(flds)
+                # per check point: are those fields the same for every (guarded) process (one tuple)?
+                key = tuple(flds) if gcode is None else (tuple(flds), gcode)
                 if key not in self.tup_sets:
                     self.tup_sets[key] = f"tu{len(self.tup_sets)}"
                 self.tup_used.add(key)
-                return (f"spec::quant_tup_c<W, {mode}>(x, {self.tup_sets[key]}, [&]({params}) -> int32_t "
+                fn = "quant_tup_c" if gcode is None else "quant_tup_gc"
+                return (f"spec::{fn}<W, {mode}>(x, {self.tup_sets[key]}, [&]({params}) -> int32_t "
                         f"{{ return {body}; }}, {fl})"), lane
             self.names[q.var.uid] = (v, False, False)
             body, lane = self.gen(q.body, in_lane, vi_depth)
@@ -1087,6 +1096,20 @@ def _tuple_fields(q):
     return out if len(out) <= 4 else None
 
 
+def _tuple_guard(q):
+    """Conjuncts A of forall(j => A && .. ==> B) / exists, count(j => A && .. && B) that read
+    only j's fields (no quantifier, set or other variable): the processes where one fails
+    contribute nothing, so the distinct-state walk visits only those where all hold."""
+    uid = q.var.uid
+    if q.kind == "forall":
+        if not (isinstance(q.body, Bin) and q.body.op == "IMPL"):
+            return []
+        cs = _conjuncts(q.body.x)
+    else:
+        cs = _conjuncts(q.body)
+    return [c for c in cs if _free_vars(c) == {uid} and not _expensive(c)]
+
+
 def _conjuncts(e):
     if isinstance(e, Bin) and e.op == "AND":
         return _conjuncts(e.x) + _conjuncts(e.y)
@@ -1276,28 +1299,42 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
         visit(rt)
 
     def tup_decls(used, ind):
-        return [f"{ind}const auto {gen.tup_sets[k]} = spec::tup_uniform<W>(x, "
-                + ", ".join(f"spec::Fld<{f}, {tag}>{{}}" for f, tag in k) + ");"
-                for k in gen.tup_sets if k in used]
+        out = []
+        for k in gen.tup_sets:
+            if k not in used:
+                continue
+            flds, gcode = (k, None) if not (len(k) == 2 and isinstance(k[1], str)) else k
+            fl = ", ".join(f"spec::Fld<{f}, {tag}>{{}}" for f, tag in flds)
+            if gcode is None:
+                out.append(f"{ind}const auto {gen.tup_sets[k]} = spec::tup_uniform<W>(x, {fl});")
+            else:
+                out.append(f"{ind}const auto {gen.tup_sets[k]} = spec::tup_uniform_g<W>(x, {gcode}, {fl});")
+        return out
 
     def block(uni):
         """The slot lines of fail() and the Termination expression, under the general or the
-        symmetric-check-point lowering."""
+        symmetric-check-point lowering. A distinct-state tuple test is declared just before the
+        first line that uses it (short live ranges: the fused kernels are register-bound)."""
         gen.uni, gen.cse, gen.tup_used = uni, {}, set()
         ind, pre = ("      ", "ucse") if uni else ("    ", "cse")
         lines = []
+
+        def add(e, fmt):
+            before = set(gen.tup_used)
+            c, _ = gen.gen(e, False, 0)
+            lines.extend(tup_decls(gen.tup_used - before, ind))
+            lines.append(fmt(c))
+
         slot = 0
         for e in order:
             if seen[_skey(e, gen.skeys)] > 1 and isinstance(e, (Quant, Contains)) and not _free_vars(e):
-                c, _ = gen.gen(e, False, 0)
                 name = f"{pre}{len(gen.cse)}"
-                lines.append(f"{ind}const int32_t {name} = {c};")
+                add(e, lambda c, name=name: f"{ind}const int32_t {name} = {c};")
                 gen.cse[_skey(e, gen.skeys)] = name
         iv = "uinv" if uni else "inv"
         if invs:
             for k, inv in enumerate(invs):
-                c, _ = gen.gen(inv, False, 0)
-                lines.append(f"{ind}const int32_t {iv}{k} = {c};")
+                add(inv, lambda c, k=k: f"{ind}const int32_t {iv}{k} = {c};")
             lines.append(f"{ind}if (!(" + " | ".join(f"({iv}{k} != 0)" for k in range(len(invs)))
                          + f")) fb |= 1u << {slot};")
             slot += 1
@@ -1312,15 +1349,13 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
                 term, _ = gen.gen(f, False, 0)
                 term_tups, gen.tup_used = gen.tup_used, saved
                 continue
-            c, _ = gen.gen(f, False, 0)
-            lines.append(f"{ind}if (({c}) == 0) fb |= 1u << {slot};  // {name}")
+            add(f, lambda c, slot=slot, name=name: f"{ind}if (({c}) == 0) fb |= 1u << {slot};  // {name}")
             slot += 1
         if safety is not None:
-            c, _ = gen.gen(safety, False, 0)
-            lines.append(f"{ind}if (({c}) == 0) fb |= 1u << {slot};  // SafetyPredicate")
+            add(safety, lambda c, slot=slot: f"{ind}if (({c}) == 0) fb |= 1u << {slot};  // SafetyPredicate")
             slot += 1
         assert slot == len(prog.slot_entry)
-        return tup_decls(gen.tup_used, ind) + lines, term, tup_decls(term_tups, ind), slot
+        return lines, term, tup_decls(term_tups, ind), slot
 
     lines, term, term_decls, slot = block(False)
     # symmetric check points (every process holds the same value of each current / old field

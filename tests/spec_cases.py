@@ -134,6 +134,23 @@ def symmetric_shapes():
     ])
 
 
+def guard_shapes():
+    """Guarded distinct-state quantifiers (spec::quant_tup_gc): nested forall(j => A(j) ==> B),
+    exists / count(j => A(j) && B) with A on j's current / old fields, several guard conjuncts,
+    a guard no process meets (the quantifier's identity) and a guard mixed with the outer
+    variable (only j's conjuncts guard)."""
+    return F.Spec(properties=[
+        ("GForall", P.forall(lambda i: P.forall(lambda j: (j.decided & (j.x > 0) & i.decided).implies(
+            j.decision == i.decision)))),
+        ("GExists", P.forall(lambda i: P.exists(lambda j: j.decided & (j.decision == i.x)) | ~i.decided)),
+        ("GCount", P.forall(lambda i: (P.filter(lambda j: j.decided & (j.decision == i.decision)).size >= 1)
+                            | ~i.decided)),
+        ("GEmpty", P.forall(lambda i: P.forall(lambda j: (j.x < -5).implies(j.decision == i.x + 7)))),
+        ("GEmptyCount", P.exists(lambda i: P.filter(lambda j: (j.x < -5) & (j.x == i.x)).size == 0)),
+        ("GOld", P.exists(lambda i: P.forall(lambda j: old(j.decided).implies(j.decided & (j.x >= i.x - 100))))),
+    ])
+
+
 # (id, algorithm, n, make_config kwargs, spec factory)
 CUSTOM = [
     ("fm-n12", psync.FloodMin(2), 12, dict(value_range=8, schedule=H(drop_log2=0, good_round=0.0, crash_fmax=3)),
@@ -171,4 +188,11 @@ CUSTOM = [
     ("lv-n8-v1-sym", psync.LastVoting(), 8, dict(value_range=1), lv_custom),
     ("fm-n8-sym", psync.FloodMin(2), 8, dict(value_range=2, schedule=H(drop_log2=0, good_round=0.0,
                                                                         crash_fmax=3)), symmetric_shapes),
+    # guarded tuple quantifiers: crashed / undecided processes outside the guard set
+    ("otr-n16-guard", psync.OTR(), 16, dict(value_range=3), guard_shapes),
+    ("fm-n12-guard", psync.FloodMin(2), 12, dict(value_range=4, schedule=H(drop_log2=0, good_round=0.0,
+                                                                            crash_fmax=3)), guard_shapes),
+    ("lv-n8-guard", psync.LastVoting(), 8, dict(value_range=3, schedule=H(drop_log2=1, good_round=0.0,
+                                                                           crash_fmax=3)), guard_shapes),
+    ("otr2-n100-guard", psync.OTR2(), 100, dict(value_range=3), guard_shapes),
 ]
