@@ -187,3 +187,27 @@ def test_fused_lowering_builds(alg):
     src = F._fused_source(alg, [1]) + F.codegen_hip(spec, alg)[0]  # what the module was built from
     assert f"psg_fused_a{alg}_w1" in src and f"psg_fused_x_a{alg}_w1" in src
     assert f"psg_spec_alg = {alg};" in src and prog.alg == alg
+
+
+def test_symmetric_and_guard_classification():
+    """The shape analyses behind the symmetric-check-point lowering (_symmetric: a process
+    variable read only through current / old fields) and the guarded distinct-state walk
+    (_tuple_guard: the conjuncts that read only the quantified process)."""
+    P, init, old = F.P, F.init, F.old
+
+    def q(mk):
+        e = mk()
+        assert isinstance(e, F.Quant)
+        return e
+    assert F._symmetric(q(lambda: P.forall(lambda i: i.decided.implies(i.decision == old(i.decision)))))
+    assert not F._symmetric(q(lambda: P.forall(lambda i: i.x == init(i.x))))  # reads init
+    A = P.filter(lambda i: i.decided)
+    assert not F._symmetric(q(lambda: P.forall(lambda i: A.contains(i))))  # used as a pid
+    # forall(j => A(j) ==> B): the conjuncts of A reading only j
+    g = F._tuple_guard(q(lambda: P.forall(lambda j: (j.decided & (j.x > 0)).implies(j.decision == 3))))
+    assert len(g) == 2
+    outer = F.Var("proc")
+    g = F._tuple_guard(q(lambda: P.forall(lambda j: (outer.decided & j.decided).implies(j.decision == outer.x))))
+    assert len(g) == 1  # outer.decided reads another process
+    assert F._tuple_guard(q(lambda: P.exists(lambda j: j.decided & (j.decision == outer.x)))) != []
+    assert F._tuple_guard(q(lambda: P.forall(lambda j: j.decided & (j.decision == 1)))) == []  # not an implication
