@@ -352,12 +352,67 @@ bool count_guard(const Tree& T, int q, CountGuard& g) {
   return false;
 }
 
-// V.exists(v => A && B(v)) -> A && V.exists(v => B(v)) for the conjuncts A free of v (formula.py
-// _rewrite_vint / _vint_step, shared subformulas stay shared)
+// e reads a field of a process other than uid, or holds a quantifier / set membership
+// (formula.py _cross)
+bool cross(const Tree& T, int e, int uid) {
+  std::vector<int> w;
+  T.walk(e, w);
+  for (int x : w) {
+    const Node& n = T.nodes[x];
+    if (n.k == QUANT || n.k == CONTAINS) return true;
+    if (n.k == FIELD && !is_var(T, n.a, uid)) return true;
+  }
+  return false;
+}
+
+// V.exists(v => A && B(v)) -> A && V.exists(v => B(v)) for the conjuncts A free of v, a conjunct
+// P.forall(i => A && B) split into P.forall(A) && P.forall(B) first, A the conjuncts free of v
+// doing cross-lane work (formula.py _rewrite_vint / _split_forall / _vint_step, shared
+// subformulas stay shared)
+// the conjuncts of quantifier q's body, each P.forall(i => A && B) among them split into
+// P.forall(A), P.forall(B): A the conjuncts free of q's variable (and doing cross-lane work,
+// cross_only) (formula.py _split_forall)
+void split_conjuncts(Tree& T, int q, bool cross_only, std::vector<int>& cs) {
+  const int uid = T.nodes[q].uid;
+  std::vector<int> cs0;
+  conjuncts(T, T.nodes[q].a, cs0);
+  for (int c : cs0) {
+    const Node C = T.nodes[c];
+    if (C.k == QUANT && C.qk == QFORALL) {
+      std::vector<int> ds, dfr, dbd;
+      conjuncts(T, C.a, ds);
+      for (int d : ds) (!free_of(T, d).count(uid) && (!cross_only || cross(T, d, C.uid)) ? dfr : dbd).push_back(d);
+      if (!dfr.empty() && !dbd.empty()) {
+        const int a = and_all(T, dfr);
+        cs.push_back(T.quant(QFORALL, C.uid, a));
+        const int b = and_all(T, dbd);
+        cs.push_back(T.quant(QFORALL, C.uid, b));
+        continue;
+      }
+    }
+    cs.push_back(c);
+  }
+}
+
+// P.exists(j => A && B(j)) -> A && P.exists(j => B(j)), the same for P.forall (n >= 1), for the
+// conjuncts A free of j (formula.py _proc_step)
+int proc_step(Tree& T, int q) {
+  const int uid = T.nodes[q].uid, qk = T.nodes[q].qk;
+  std::vector<int> cs, fr, bd;
+  split_conjuncts(T, q, false, cs);
+  for (int c : cs) (free_of(T, c).count(uid) ? bd : fr).push_back(c);
+  if (!fr.empty() && !bd.empty()) {
+    std::vector<int> all = fr;
+    all.push_back(T.quant(qk, uid, and_all(T, bd)));
+    return and_all(T, all);
+  }
+  return q;
+}
+
 int vint_step(Tree& T, int q) {
   const int uid = T.nodes[q].uid;
   std::vector<int> cs, fr, bd;
-  conjuncts(T, T.nodes[q].a, cs);
+  split_conjuncts(T, q, true, cs);
   for (int c : cs) (free_of(T, c).count(uid) ? bd : fr).push_back(c);
   if (!fr.empty() && !bd.empty()) {
     std::vector<int> all = fr;
@@ -376,6 +431,7 @@ int rewrite_vint(Tree& T, int e, std::map<int, int>& memo) {
     const int b = rewrite_vint(T, n.a, memo);
     out = b == n.a ? e : T.quant(n.qk, n.uid, b);
     if (T.nodes[out].qk == QVINT) out = vint_step(T, out);
+    else if (T.nodes[out].qk == QEXISTS || T.nodes[out].qk == QFORALL) out = proc_step(T, out);
   } else if (n.k == BIN) {
     const int x = rewrite_vint(T, n.a, memo);
     const int y = rewrite_vint(T, n.b, memo);
@@ -554,6 +610,9 @@ struct Gen {
     if (Q.qk == QFORALL || Q.qk == QEXISTS || Q.qk == QCOUNT) {
       const int mode = Q.qk == QFORALL ? 0 : Q.qk == QEXISTS ? 1 : 2;
       pvars.insert(Q.uid);
+      // a variable may be bound by several quantifiers (split_conjuncts): drop its last binding
+      tuples.erase(Q.uid);
+      names.erase(Q.uid);
       if (uni) {
         Code got;
         if (quant_uni(q, v, in_lane, vi, got)) return got;

@@ -804,6 +804,9 @@ class _Gen:
         v = f"v{next(self.k)}"
         if q.kind in ("forall", "exists", "count"):
             self.pvars.add(q.var.uid)
+            # a variable may be bound by several quantifiers (_split_forall): drop its last binding
+            self.tuples.pop(q.var.uid, None)
+            self.names.pop(q.var.uid, None)
             if self.uni:
                 got = self._quant_uni(q, v, in_lane, vi_depth)
                 if got is not None:
@@ -1206,7 +1209,9 @@ def _rewrite_vint(e, memo=None):
     domain is non-empty and both sides are decided exactly):
       V.exists(v => V.exists(t => B)) -> V.exists(t => V.exists(v => B)) when v has equality
         pins in B and t has none (the pinned variable innermost, where one candidate decides it);
-      V.exists(v => A && B(v)) -> A && V.exists(v => B(v)) for the conjuncts A free of v.
+      V.exists(v => A && B(v)) -> A && V.exists(v => B(v)) for the conjuncts A free of v,
+        P.forall conjuncts split first (_split_forall: LastVoting's majority clause evaluates
+        its v- and t-free implications once, not per candidate).
     Shared subformulas stay shared (memo by object)."""
     memo = {} if memo is None else memo
     k = id(e)
@@ -1222,6 +1227,8 @@ def _rewrite_vint(e, memo=None):
         out = e if b is e.body else Quant(e.kind, e.var, b)
         if out.kind == "vint":
             out = _vint_step(out, memo)
+        elif out.kind in ("exists", "forall") and SPLIT_FORALL:
+            out = _proc_step(out)
     elif isinstance(e, Bin):
         x, y = _rewrite_vint(e.x, memo), _rewrite_vint(e.y, memo)
         out = e if (x is e.x and y is e.y) else Bin(e.op, x, y)
@@ -1235,9 +1242,54 @@ def _rewrite_vint(e, memo=None):
     return out
 
 
+# V.exists(v => ... && P.forall(i => A(i) && B(i, v)) && ...): the forall splits into
+# P.forall(A) && P.forall(B) so that A, free of v, leaves the quantifier (_vint_step) when A
+# does cross-lane work (reads another process's field: LastVoting's coord.commit); A of the
+# lane's own fields stays in the forall (a separate forall would cost one more ballot than it
+# saves). Off only for A/B measurements (psg_spec_gen.cpp always splits).
+SPLIT_FORALL = True
+
+
+def _cross(d, uid):
+    """d reads a field of a process other than `uid`, or holds a quantifier / set membership."""
+    for x in _walk(d):
+        if isinstance(x, (Quant, Contains)):
+            return True
+        if isinstance(x, Field) and not (isinstance(x.proc, Var) and x.proc.uid == uid):
+            return True
+    return False
+
+
+def _split_forall(c, v, cross_only=True):
+    """P.forall(i => A && B) with conjuncts A free of v (and doing cross-lane work, cross_only)
+    and the rest B -> [P.forall(A), P.forall(B)] (forall distributes over &&: exact)."""
+    if SPLIT_FORALL and isinstance(c, Quant) and c.kind == "forall":
+        ds = _conjuncts(c.body)
+        out = [v not in _free_vars(d) and (not cross_only or _cross(d, c.var.uid)) for d in ds]
+        fr = [d for d, o in zip(ds, out) if o]
+        bd = [d for d, o in zip(ds, out) if not o]
+        if fr and bd:
+            return [Quant("forall", c.var, And(*fr)), Quant("forall", c.var, And(*bd))]
+    return [c]
+
+
+def _proc_step(q):
+    """P.exists(j => A && B(j)) -> A && P.exists(j => B(j)), the same for P.forall (n >= 1: exact),
+    for the conjuncts A free of j, a conjunct P.forall(i => A(i) && B(i, j)) split first
+    (LastVoting's / OTR's P.exists(j => P.forall(i => i.decided && i.decision == init(j.x))):
+    the serial walk over i runs only once every process decided)."""
+    v = q.var.uid
+    cs = [d for c in _conjuncts(q.body) for d in _split_forall(c, v, cross_only=False)]
+    free = [c for c in cs if v not in _free_vars(c)]
+    bound = [c for c in cs if v in _free_vars(c)]
+    if free and bound:
+        return And(*free, Quant(q.kind, q.var, And(*bound)))
+    return q
+
+
 def _vint_step(q, memo):
     v, body = q.var.uid, q.body
-    cs = _conjuncts(body)
+    cs = [d for c in _conjuncts(body) for d in _split_forall(c, v)]
     free = [c for c in cs if v not in _free_vars(c)]
     bound = [c for c in cs if v in _free_vars(c)]
     if free and bound:

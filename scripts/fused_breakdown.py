@@ -4,7 +4,7 @@ fused modules that evaluate one formula of OTR.spec at a time (plus an empty Spe
 round kernel alone), kernel time per launch. Compile here (native modules are cached under
 build/spec and travel with the tree), run on the GPU box.
 
-usage: fused_breakdown.py [--compile-only] [--instances N] [--alg otr|lv] [--nosym]
+usage: fused_breakdown.py [--compile-only] [--instances N] [--alg otr|lv] [--nosym] [--nosplit]
 (--nosym: modules without the symmetric-check-point lowering, formula.SYMMETRIC_LOWERING)
 """
 import argparse
@@ -48,11 +48,13 @@ def main():
     ap.add_argument("--instances", type=int, default=2_500_000)
     ap.add_argument("--alg", default="otr")
     ap.add_argument("--nosym", action="store_true")
+    ap.add_argument("--nosplit", action="store_true", help="modules without formula.SPLIT_FORALL")
     ap.add_argument("--timers", action="store_true",
                     help="profiling modules (-DPSG_PHASE_TIMERS=1) of the full Spec and the round kernel alone; "
                          "run with PSG_LIB=round_amd/libpsg_timers.so PSG_PHASE_TIMERS=1")
     args = ap.parse_args()
     F.SYMMETRIC_LOWERING = not args.nosym
+    F.SPLIT_FORALL = not args.nosplit
     if args.alg == "otr":
         alg, aid, kw, variants = psync.OTR(), abi.PSG_ALG_OTR, dict(value_range=64), otr_variants()
     else:
@@ -73,7 +75,7 @@ def main():
         for k, p in progs.items():
             g.run_spec(0, I, p)
             t = [g.run_spec(0, I, p).summary.kernel_ns for _ in range(2)]
-            print(json.dumps({"variant": k, "symmetric": not args.nosym, "kernel_ms": min(t) / 1e6}), flush=True)
+            print(json.dumps({"variant": k, "symmetric": not args.nosym, "split": not args.nosplit, "kernel_ms": min(t) / 1e6}), flush=True)
 
 
 if __name__ == "__main__":
