@@ -151,6 +151,31 @@ def guard_shapes():
     ])
 
 
+def split_shapes():
+    """Split foralls and hoisted conjuncts (formula._split_forall / _proc_step / _vint_step):
+    a conjunct free of the outer variable leaves a process quantifier (exists and forall, the
+    inner variable then bound twice, once by the hoisted lane-level forall and once by the walk
+    left inside), a cross-lane conjunct (coord's field, a nested count) leaves V.exists, and the
+    split under an implication / disjunction (no hoisting there)."""
+    c = F.coord
+    cdec = F.Field(F.FIELD_DECIDED, c)
+    return F.Spec(properties=[
+        ("SplitExists", P.exists(lambda j: P.forall(lambda i: i.decided & (i.decision >= j.x - 1))) | (r < 3)),
+        ("SplitForall", P.forall(lambda j: P.forall(lambda i: (i.x >= -100) & (i.x != j.x + 100)))),
+        ("SplitMixed", P.exists(lambda j: (r > 0) & P.forall(lambda i: cdec.implies(i.decided)
+                                                             & i.decided.implies(i.decision <= j.x + 2)))
+         | (r < 4)),
+        ("SplitCount", P.exists(lambda j: P.forall(lambda i: (P.filter(lambda k: k.x == i.x).size >= 1)
+                                                   & (i.x >= j.x - 1)))),
+        ("SplitVint", V.exists(lambda v: P.forall(lambda i: cdec.implies(i.decided)
+                                                  & i.decided.implies(i.decision == v))) | (r < 5)),
+        ("SplitVint2", V.exists(lambda v: V.exists(lambda t: (P.filter(lambda i: i.x >= t).size > n // 2)
+                                                   & P.forall(lambda i: (i.x >= t).implies(i.x == v)
+                                                              & (c.x >= -100)))) | (r < 2)),
+        ("SplitUnder", P.forall(lambda j: j.decided.implies(P.exists(lambda i: i.decided & (i.decision == j.decision))))),
+    ])
+
+
 # (id, algorithm, n, make_config kwargs, spec factory)
 CUSTOM = [
     ("fm-n12", psync.FloodMin(2), 12, dict(value_range=8, schedule=H(drop_log2=0, good_round=0.0, crash_fmax=3)),
@@ -195,4 +220,12 @@ CUSTOM = [
     ("lv-n8-guard", psync.LastVoting(), 8, dict(value_range=3, schedule=H(drop_log2=1, good_round=0.0,
                                                                            crash_fmax=3)), guard_shapes),
     ("otr2-n100-guard", psync.OTR2(), 100, dict(value_range=3), guard_shapes),
+    # split foralls / hoisted conjuncts
+    ("otr-n16-split", psync.OTR(), 16, dict(value_range=3), split_shapes),
+    ("fm-n12-split", psync.FloodMin(2), 12, dict(value_range=4, schedule=H(drop_log2=0, good_round=0.0,
+                                                                            crash_fmax=3)), split_shapes),
+    ("lv-n8-split", psync.LastVoting(), 8, dict(value_range=3, schedule=H(drop_log2=1, good_round=0.0,
+                                                                           crash_fmax=3)), split_shapes),
+    ("fm-n100-split", psync.FloodMin(2), 100, dict(value_range=4, schedule=H(drop_log2=0, good_round=0.0,
+                                                                              crash_fmax=3)), split_shapes),
 ]
