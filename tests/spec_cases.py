@@ -221,11 +221,11 @@ CUSTOM = [
                                                                            crash_fmax=3)), guard_shapes),
     ("otr2-n100-guard", psync.OTR2(), 100, dict(value_range=3), guard_shapes),
     # split foralls / hoisted conjuncts
-    ("otr-n8-split", psync.OTR(), 8, dict(value_range=3), split_shapes),
+    ("otr-n16-split", psync.OTR(), 16, dict(value_range=3), split_shapes),
     ("fm-n12-split", psync.FloodMin(2), 12, dict(value_range=4, schedule=H(drop_log2=0, good_round=0.0,
                                                                             crash_fmax=3)), split_shapes),
-    ("lv-n6-split", psync.LastVoting(), 6, dict(value_range=3, schedule=H(drop_log2=1, good_round=0.0,
-                                                                           crash_fmax=2)), split_shapes),
+    ("lv-n8-split", psync.LastVoting(), 8, dict(value_range=3, schedule=H(drop_log2=1, good_round=0.0,
+                                                                           crash_fmax=3)), split_shapes),
     ("fm-n100-split", psync.FloodMin(2), 100, dict(value_range=4, schedule=H(drop_log2=0, good_round=0.0,
                                                                               crash_fmax=3)), split_shapes),
 ]
