@@ -95,12 +95,33 @@ def _free_port():
         return so.getsockname()[1]
 
 
+def visible_gpus(env=None):
+    """GPUs the ranks can see, counted WITHOUT the HIP runtime (hipGetDeviceCount would
+    initialise HSA in this parent and keep a KFD context open for the whole run): the
+    *_VISIBLE_DEVICES list when one is set, else the KFD topology nodes that have SIMDs.
+    None when neither is readable (the ranks then report a missing device themselves)."""
+    env = os.environ if env is None else env
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if env.get(var, "").strip():
+            return len([d for d in env[var].split(",") if d.strip()])
+    nodes = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        count = 0
+        for node in os.listdir(nodes):
+            with open(os.path.join(nodes, node, "properties")) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            count += int(props.get("simd_count", "0")) > 0
+        return count
+    except OSError:
+        return None
+
+
 def launch_ranks(argv, nproc, dry_run):
-    """Start `nproc` ranks as a child process and return its exit code. Runs before any
-    GPU call in this process (counting devices does not initialise the GPU here)."""
+    """Start `nproc` ranks as a child process and return its exit code. Nothing in this
+    process touches the GPU: the device count comes from visible_gpus(), not from HIP."""
     if not dry_run:
-        have = torch.cuda.device_count()
-        if have < nproc:
+        have = visible_gpus()
+        if have is not None and have < nproc:
             raise SystemExit(f"bench.py: --gpus {nproc} needs {nproc} visible GPUs, {have} found "
                              "(--device-list runs several contexts in one process instead)")
     env = dict(os.environ)

@@ -797,16 +797,22 @@ struct KSet {
       s.decided = true; s.decision = pick(s.t);
       return true;
     }
-    bool anyDecider = false;
+    /* val content = mailbox.map{ case (k,v) => v } (KSetAgreement.scala:47): v is a pair
+     * (Boolean, Map[ProcessID,Int]), so Scala 2.13 picks MapOps.map[K2,V2] and content is a
+     * Map[Boolean, Map[ProcessID,Int]] built by inserting every message in the mailbox's
+     * iteration order; a later message with the same flag overwrites the value. Hence
+     * content.find(_._1).get._2 (:53) is the t of the LAST decider in iteration order. */
+    bool anyDecider = false; /* content.exists(_._1) (:51) */
     for (auto& m : mb) anyDecider = anyDecider || m.payload.decider;
-    if (anyDecider) { /* content.find(_._1): first in Map iteration order */
+    if (anyDecider) {
       std::vector<int> ins;
       for (auto& m : mb) ins.push_back(m.src);
-      for (int q : scala_map_order(ins, tiebreak)) {
-        const Msg<Payload>* mm = nullptr;
-        for (auto& m : mb) if (m.src == q) mm = &m;
-        if (mm->payload.decider) { s.decider = true; s.t = *mm->payload.t; break; }
-      }
+      std::map<bool, std::shared_ptr<const std::map<int, int32_t>>> content;
+      for (int q : scala_map_order(ins, tiebreak))
+        for (auto& m : mb)
+          if (m.src == q) content[m.payload.decider] = m.payload.t;
+      s.decider = true;
+      s.t = *content.at(true);
     } else {
       int same = 0;
       for (auto& m : mb) if (*m.payload.t == s.t) ++same;

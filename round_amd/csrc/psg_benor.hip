@@ -274,7 +274,7 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
     const bool pred = !(flags & 256u);
     ck.record(fbit(inv0, 0) | fbit(inv0, 1) | fbit(same, 2) | fbit(irrev, 3) | fbit(pred, 4), cntD == n, c, P.lane);
   };
-  check(0, false, std::integral_constant<int, 0>{});
+  check(0, false, Slot<0>{});
   // one round of slot RS = k & 1 (compile time: the R0 / R1 step and the next check specialized)
   auto round = [&](const int k, auto RSc) {
     constexpr int RS = decltype(RSc)::value;
@@ -339,11 +339,11 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
         if (halt_round[j] == k) halted[j] = 1;
       }
     }
-    check(k + 1, true, std::integral_constant<int, (RS + 1) & 1>{});
+    check(k + 1, true, Slot<(RS + 1) & 1>{});
   };
   for (int k0 = 0; k0 < a.R; k0 += 2) {
-    round(k0, std::integral_constant<int, 0>{});
-    if (k0 + 1 < a.R) round(k0 + 1, std::integral_constant<int, 1>{});
+    round(k0, Slot<0>{});
+    if (k0 + 1 < a.R) round(k0 + 1, Slot<1>{});
   }
   int32_t fx[W];
 #pragma unroll

@@ -32,6 +32,13 @@ using __hip_internal::uint64_t;
 
 namespace psg {
 
+// A compile-time phase slot passed to a generic lambda (the round loops specialise each slot's
+// step): a tag of our own, since hiprtc (psg_spec_compile_native) has no <type_traits>
+template <int K>
+struct Slot {
+  static constexpr int value = K;
+};
+
 // ---------------------------------------------------------------- kernel args
 struct KArgs {
   uint64_t inst_begin;
@@ -420,6 +427,14 @@ PSG_DEV int mfirst(const Mask<W>& a) {
 #pragma unroll
   for (int i = 0; i < W; ++i)
     if (a.w[i]) return i * 64 + __builtin_ctzll(a.w[i]);
+  return -1;
+}
+// last set pid (-1 if empty)
+template <int W>
+PSG_DEV int mlast(const Mask<W>& a) {
+#pragma unroll
+  for (int i = W - 1; i >= 0; --i)
+    if (a.w[i]) return i * 64 + 63 - __builtin_clzll(a.w[i]);
   return -1;
 }
 template <int W>

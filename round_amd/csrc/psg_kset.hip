@@ -6,7 +6,7 @@
 // initial vector: a W x 64-bit mask per process; `t == t'` is mask equality,
 // `t ++ t'` is OR, pick(t) = min of the initial values of the origins (40).
 // Payloads (decider, t) are staged in LDS; each process walks the alive senders
-// with broadcast LDS reads. `content.find(_._1)` (53) takes the first decider
+// with broadcast LDS reads. `content.find(_._1)` (47-53) takes the LAST decider
 // message in Scala Map iteration order (CHAMP for > 4 entries).
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
@@ -51,15 +51,18 @@ PSG_DEV Mask<W> load_t(const uint64_t* ts, int q) {
   return m;
 }
 
-// `content.find(_._1)` of receiver p (KSetAgreement.scala:53): the first decider message in
-// Scala Map iteration order — the first pid of cand up to 4 mailbox entries (Map1..Map4)
-// or when the candidates agree on t; otherwise the CHAMP order's first (min sort key).
+// `content.find(_._1).get._2` of receiver p (KSetAgreement.scala:47-53). `content =
+// mailbox.map{ case (k,v) => v }` maps to pairs, so it is a Map[Boolean, Map[ProcessID,Int]]
+// built in the mailbox's iteration order, each decider message overwriting key `true`: the
+// adopted t is the LAST decider message's in Scala Map iteration order — the last pid of cand
+// up to 4 mailbox entries (Map1..Map4), under PSG_TIE_MIN_PID, or when the candidates agree
+// on t; otherwise the CHAMP order's last (max sort key).
 // hol / ncols (optional): the round's holder columns (kset_packed): the candidates' t agree
 // iff every column holds all of them or none, so no candidate's t is read.
 template <int W, int CS = 0>
 PSG_DEV int kset_find(const KArgs& a, const uint64_t* ts, const Mask<W>& M, const Mask<W>& cand,
                       const uint64_t (*hol)[W] = nullptr, int ncols = 0) {
-  int qs = mfirst(cand);
+  int qs = mlast(cand);
   if (a.tiebreak == PSG_TIE_CHAMP && mpopc(M) > 4 && mpopc(cand) > 1) {
     bool differ = false;
     if (hol) {
@@ -82,7 +85,7 @@ PSG_DEV int kset_find(const KArgs& a, const uint64_t* ts, const Mask<W>& M, cons
       }
     }
     if (differ) {
-      uint64_t best = ~0ull;
+      uint64_t best = 0;  // max key; keys of distinct pids differ (>=: the first candidate sets qs)
 #pragma unroll
       for (int w = 0; w < W; ++w) {
         uint64_t m = cand.w[w];
@@ -101,7 +104,7 @@ PSG_DEV int kset_find(const KArgs& a, const uint64_t* ts, const Mask<W>& M, cons
             }
           }
           const uint64_t key = champ_key(hq, depth);
-          if (key < best) {
+          if (key >= best) {
             best = key;
             qs = q;
           }
@@ -370,7 +373,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
             else tnew = uni;
           }
         }
-        if (adopt) {  // t = content.find(_._1).get._2 — first decider message in iteration order
+        if (adopt) {  // t = content.find(_._1).get._2 — last decider message in iteration order
           tnew = load_t<W, 64 * W>(L.ts, kset_find<W, 64 * W>(a, L.ts, M, mand(M, Dm), cols ? L.hol : nullptr, ncols));
           becomeDec = 1;
         }
@@ -556,7 +559,7 @@ PSG_DEV void kset_body(const KArgs& a) {
           }
         }
         if (adopt) {
-          // t = content.find(_._1).get._2 — first decider message in iteration order
+          // t = content.find(_._1).get._2 — last decider message in iteration order
           tnew = load_t<W>(ts, kset_find<W>(a, ts, M, cand));
           becomeDecider = true;
         }

@@ -389,10 +389,10 @@ PSG_DEV void lv_body(const KArgs& a) {
       pt.mark(many(act) ? 4 : 5);
     };
     for (int k0 = 0; k0 < a.R; k0 += 4) {
-      round(k0, std::integral_constant<int, 0>{});
-      if (k0 + 1 < a.R) round(k0 + 1, std::integral_constant<int, 1>{});
-      if (k0 + 2 < a.R) round(k0 + 2, std::integral_constant<int, 2>{});
-      if (k0 + 3 < a.R) round(k0 + 3, std::integral_constant<int, 3>{});
+      round(k0, Slot<0>{});
+      if (k0 + 1 < a.R) round(k0 + 1, Slot<1>{});
+      if (k0 + 2 < a.R) round(k0 + 2, Slot<2>{});
+      if (k0 + 3 < a.R) round(k0 + 3, Slot<3>{});
       ++phase;
       cph = cnx;
       cnx = cnx + 1 == n ? 0 : cnx + 1;

@@ -197,6 +197,7 @@ PSG_DEV void pk_finish(const Pk<W>& P, const KArgs& a, uint64_t i, const Checks&
   }
 }
 
+#ifndef PSG_FUSED_MODULE  // host code: not part of a fused Spec module (hiprtc has no host API)
 // Blocks of packed kernels: 256 threads = 4 instances; grid = resident blocks
 // (one cached occupancy per kernel, keyed by algorithm and W).
 template <int ALG, int W>
@@ -211,5 +212,6 @@ static int pk_grid(const void* kernel, uint64_t count) {
   const uint64_t want = (count + 3) / 4;
   return (int)(want < (uint64_t)resident ? (want < 1 ? 1 : want) : (uint64_t)resident);
 }
+#endif  // PSG_FUSED_MODULE
 
 }  // namespace psg

@@ -186,9 +186,9 @@ PSG_DEV void slv_body(const KArgs& a) {
       if (tracing<SH>(a)) trace(k + 1, (fl_start & S_HALTED) ? n : hs);
     };
     for (int k0 = 0; k0 < a.R; k0 += 3) {
-      round(k0, std::integral_constant<int, 0>{});
-      if (k0 + 1 < a.R) round(k0 + 1, std::integral_constant<int, 1>{});
-      if (k0 + 2 < a.R) round(k0 + 2, std::integral_constant<int, 2>{});
+      round(k0, Slot<0>{});
+      if (k0 + 1 < a.R) round(k0 + 1, Slot<1>{});
+      if (k0 + 2 < a.R) round(k0 + 2, Slot<2>{});
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 2, dec_val, dec_round, halt_round, x, &bc);
   }

@@ -960,12 +960,17 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
     std::set<Gen::TupKey> term_tups;
     for (auto& p : props) {
       if (p.first == "Termination") {
+        // term() is its own function: fail()'s hoisted subformulas (cse*) and tuple tests are
+        // not in scope there, so it is lowered with neither
         auto saved = gen.tup_used;
         gen.tup_used.clear();
+        auto saved_cse = gen.cse;
+        gen.cse.clear();
         B.term = gen.gen(p.second, false, 0).first;
         B.has_term = true;
         term_tups = gen.tup_used;
         gen.tup_used = saved;
+        gen.cse = saved_cse;
         continue;
       }
       add(p.second, [&](const std::string& c) {

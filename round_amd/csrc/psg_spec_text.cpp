@@ -9,6 +9,7 @@
 // word); slot assembly follows psync/verification/Verifier.scala:111-141 (Safety = some
 // invariant, invariant i guarded by roundInvariants(j-1)(0), properties, Termination
 // as a round, SafetyPredicate).
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -148,9 +149,9 @@ struct Lower {
     auto arg = [&](size_t k) { return expr(s.at(2 + k), env); };
     if (sym == "And" || sym == "Or") {
       if (na < 1) throw SpecError("Formula text: empty " + sym);
-      int out = arg(0);
-      for (size_t k = 1; k < na; ++k) out = T.bin(sym == "And" ? PSG_OP_AND : PSG_OP_OR, out, arg(k));
-      return out;
+      std::vector<int> xs;
+      for (size_t k = 0; k < na; ++k) xs.push_back(arg(k));
+      return fold(sym == "And" ? PSG_OP_AND : PSG_OP_OR, xs, 0, xs.size());
     }
     auto bn = bin_names().find(sym);
     if (bn != bin_names().end()) {
@@ -204,6 +205,21 @@ struct Lower {
       return T.add(n);
     }
     throw SpecError("Formula text: unknown symbol " + sym + "/" + std::to_string(na));
+  }
+
+  // An n-ary And / Or: left-deep (the DSL's `a & b & c` shape) up to kLeftFold arguments,
+  // halves folded recursively above that, so a wide conjunction stays shallow (depth
+  // kLeftFold + log2(arity)) for the recursive lowering and generator passes
+  static constexpr size_t kLeftFold = 32;
+  int fold(int op, const std::vector<int>& xs, size_t lo, size_t hi) {
+    if (hi - lo > kLeftFold) {
+      const size_t mid = lo + (hi - lo) / 2;
+      const int x = fold(op, xs, lo, mid);
+      return T.bin(op, x, fold(op, xs, mid, hi));
+    }
+    int out = xs[lo];
+    for (size_t k = lo + 1; k < hi; ++k) out = T.bin(op, out, xs[k]);
+    return out;
   }
 
   int binder(bool forall, const Sx& decls, size_t k, const Sx& body, const Env& env) {
@@ -273,9 +289,9 @@ struct Lower {
           for (size_t j = 0; j < conj.size(); ++j)
             if (j != k) rest.push_back(conj[j]);
           if (rest.empty()) return T.lit(1);
-          int out = expr(*rest[0], e2);
-          for (size_t j = 1; j < rest.size(); ++j) out = T.bin(PSG_OP_AND, out, expr(*rest[j], e2));
-          return out;
+          std::vector<int> xs;
+          for (const Sx* x : rest) xs.push_back(expr(*x, e2));
+          return fold(PSG_OP_AND, xs, 0, xs.size());
         }
       }
     }
@@ -460,6 +476,8 @@ struct Compiler {
 
 }  // namespace
 
+static constexpr int kMaxTreeDepth = 1024;
+
 ParsedSpec parse_spec(const char* text) {
   Reader rd{text};
   const Sx s = rd.read();
@@ -512,6 +530,16 @@ ParsedSpec parse_spec(const char* text) {
   }
   if (guard >= 0)
     for (int& inv : invs) inv = T.bin(PSG_OP_AND, inv, guard);
+  // The lowering and the native generator recurse over the tree: bound its depth (children
+  // precede their parents in T.nodes, so one pass in index order computes every depth)
+  std::vector<int> depth(T.nodes.size(), 1);
+  for (size_t e = 0; e < T.nodes.size(); ++e) {
+    std::vector<int> ch;
+    T.children((int)e, ch);
+    for (int c : ch) depth[e] = std::max(depth[e], depth[c] + 1);
+    if (depth[e] > kMaxTreeDepth)
+      throw SpecError("Formula text: expression tree deeper than " + std::to_string(kMaxTreeDepth));
+  }
   return P;
 }
 

@@ -1397,9 +1397,13 @@ def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
         term_tups = set()
         for name, f in props:
             if name == "Termination":
+                # term() is its own function: fail()'s hoisted subformulas (cse*) and tuple
+                # tests are not in scope there, so it is lowered with neither
                 saved, gen.tup_used = gen.tup_used, set()
+                saved_cse, gen.cse = gen.cse, {}
                 term, _ = gen.gen(f, False, 0)
                 term_tups, gen.tup_used = gen.tup_used, saved
+                gen.cse = saved_cse
                 continue
             add(f, lambda c, slot=slot, name=name: f"{ind}if (({c}) == 0) fb |= 1u << {slot};  // {name}")
             slot += 1

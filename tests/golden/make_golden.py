@@ -52,7 +52,8 @@ N_RECORDS = 3
 
 
 def config_dict(cfg):
-    d = {f: getattr(cfg, f) for f, _ in abi.Config._fields_ if f != "sched"}
+    # the device list (n_devices / devices) is run plumbing, not part of a fixture
+    d = {f: getattr(cfg, f) for f, _ in abi.Config._fields_ if f not in ("sched", "n_devices", "devices")}
     d["sched"] = {f: getattr(cfg.sched, f) for f, _ in abi.Schedule._fields_}
     return d
 
@@ -101,9 +102,9 @@ def make(name):
     })
 
 
-def main():
+def main(names=None):
     oracle.build()
-    for name in FIXTURES:
+    for name in names or FIXTURES:
         fx = make(name)
         with open(os.path.join(HERE, name + ".json"), "w") as f:
             json.dump(fx, f, separators=(",", ":"))
@@ -111,4 +112,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -176,6 +176,17 @@ def split_shapes():
     ])
 
 
+def term_shared_shapes():
+    """Termination repeating a closed subformula that two other slots share (so
+    fail() hoists it as cse0 / ucse0). term() is a separate function: it must lower the
+    subformula itself instead of naming fail()'s local."""
+    return F.Spec(properties=[
+        ("Termination", P.forall(lambda i: i.decided)),
+        ("AllOrNone", P.forall(lambda i: i.decided) | (n == 0)),
+        ("AllOrOne", P.forall(lambda i: i.decided) | (n == 1)),
+    ])
+
+
 # (id, algorithm, n, make_config kwargs, spec factory)
 CUSTOM = [
     ("fm-n12", psync.FloodMin(2), 12, dict(value_range=8, schedule=H(drop_log2=0, good_round=0.0, crash_fmax=3)),
@@ -228,4 +239,8 @@ CUSTOM = [
                                                                            crash_fmax=3)), split_shapes),
     ("fm-n100-split", psync.FloodMin(2), 100, dict(value_range=4, schedule=H(drop_log2=0, good_round=0.0,
                                                                               crash_fmax=3)), split_shapes),
+    # Termination sharing a subformula hoisted in fail()
+    ("otr-n16-termcse", psync.OTR(), 16, dict(value_range=3), term_shared_shapes),
+    ("fm-n12-termcse", psync.FloodMin(2), 12, dict(value_range=4, schedule=H(drop_log2=0, good_round=0.0,
+                                                                              crash_fmax=3)), term_shared_shapes),
 ]

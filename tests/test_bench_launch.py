@@ -51,9 +51,21 @@ def test_gpus_two_spawns_two_ranks():
 
 def test_gpus_beyond_visible_devices_fails_loudly(monkeypatch):
     """Never a silent n_gpus = 1 when more were asked for."""
-    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setattr(bench, "visible_gpus", lambda env=None: 1)
     with pytest.raises(SystemExit, match="needs 4 visible GPUs"):
         bench.launch_ranks(["--gpus", "4"], 4, dry_run=False)
+
+
+def test_visible_gpus_never_initialises_hip(monkeypatch):
+    """the parent counts devices from the environment / KFD topology, not through
+    hipGetDeviceCount (which would initialise HSA before the ranks start)."""
+    def boom():
+        raise AssertionError("HIP touched in the launching parent")
+    monkeypatch.setattr(bench.torch.cuda, "device_count", boom)
+    assert bench.visible_gpus({"HIP_VISIBLE_DEVICES": "0,1,2"}) == 3
+    assert bench.visible_gpus({"ROCR_VISIBLE_DEVICES": "4"}) == 1
+    n = bench.visible_gpus({})
+    assert n is None or n >= 0
 
 
 def test_host_cores_respects_quota(monkeypatch):

@@ -164,12 +164,13 @@ def test_program_layout():
     assert all(prog.code[e - 1] & 0xFF == 0 or e == 0 for e in prog.slot_entry)  # each root follows a HALT
 
 
-@pytest.mark.parametrize("name", ["otr", "otr2", "lv", "benor", "custom"])
+@pytest.mark.parametrize("name", ["otr", "otr2", "lv", "benor", "custom", "termcse"])
 def test_native_lowering_builds(name):
     """codegen_hip output compiles for gfx950 (hipcc --genco; no GPU needed)."""
     specs = {"otr": (F.otr_spec, abi.PSG_ALG_OTR), "otr2": (F.otr2_spec, abi.PSG_ALG_OTR2),
              "lv": (F.lv_spec, abi.PSG_ALG_LAST_VOTING), "benor": (F.benor_spec, abi.PSG_ALG_BENOR),
-             "custom": (spec_cases.lv_custom, abi.PSG_ALG_LAST_VOTING)}
+             "custom": (spec_cases.lv_custom, abi.PSG_ALG_LAST_VOTING),
+             "termcse": (spec_cases.term_shared_shapes, abi.PSG_ALG_OTR)}
     mk, alg = specs[name]
     prog = F.compile_native(mk(), alg)
     import os

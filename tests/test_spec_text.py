@@ -167,3 +167,28 @@ def test_deep_nesting_is_refused_not_a_crash():
     deep = "(Spec (invariants " + "(Not " * 100000 + "true" + ")" * 100000 + "))"
     with pytest.raises(F.FormulaError, match="nesting deeper than 512"):
         lib.spec_from_text(deep, abi.PSG_ALG_OTR)
+
+
+def test_wide_conjunction_is_shallow_not_a_crash():
+    """a 100k-conjunct (App And ...) folds into a tree of depth 32 + log2(arity)
+    instead of a 100k-deep chain, so the lowering and the native generator do not overflow the
+    stack (run on a 1 MB thread, the JVM's default stack size); <= 32 arguments keep the DSL's
+    left-deep shape."""
+    import threading
+    atoms = " ".join("(App Leq (App x (Var i)) (Lit %d))" % j for j in range(100000))
+    wide = "(Spec (invariants (ForAll ((i pid)) (App And " + atoms + "))))"
+    out = {}
+
+    def run():
+        out["prog"] = lib.spec_from_text(wide, abi.PSG_ALG_OTR)
+        few = " ".join("(App Leq (App x (Var i)) (Lit %d))" % j for j in range(2000))
+        out["src"] = lib.spec_native_source(wide.replace(atoms, few), abi.PSG_ALG_OTR)
+
+    old = threading.stack_size(1 << 20)
+    try:
+        th = threading.Thread(target=run)
+        th.start()
+        th.join()
+    finally:
+        threading.stack_size(old)
+    assert out["prog"].slot_names[0] == "Safety" and "struct GenSpec" in out["src"]
