@@ -36,7 +36,6 @@ import torch.distributed as dist  # noqa: E402
 from round_amd import dist as rdist  # noqa: E402
 from round_amd import psync  # noqa: E402
 
-B_ALG_OTR = 24  # algorithmic bytes per process-round
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 CUS = 256  # MI355X compute units (8 XCDs x 32)
 
@@ -83,10 +82,11 @@ def plan(args, env):
     return "single", 1
 
 
-def launch_cmd(argv, nproc, port):
+def launch_cmd(argv, nproc, port, script=None):
     """The child torchrun command line for `launch` mode (rendezvous on 127.0.0.1)."""
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+            "--master-addr", "127.0.0.1", f"--master-port={port}",
+            os.path.abspath(script or __file__)] + list(argv)
 
 
 def _free_port():
@@ -116,9 +116,10 @@ def visible_gpus(env=None):
         return None
 
 
-def launch_ranks(argv, nproc, dry_run):
-    """Start `nproc` ranks as a child process and return its exit code. Nothing in this
-    process touches the GPU: the device count comes from visible_gpus(), not from HIP."""
+def launch_ranks(argv, nproc, dry_run, script=None):
+    """Start `nproc` ranks of `script` (default: this file) as a child process and return its
+    exit code. Nothing in this process touches the GPU: the device count comes from
+    visible_gpus(), not from HIP."""
     if not dry_run:
         have = visible_gpus()
         if have is not None and have < nproc:
@@ -126,7 +127,7 @@ def launch_ranks(argv, nproc, dry_run):
                              "(--device-list runs several contexts in one process instead)")
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.call(launch_cmd(argv, nproc, _free_port()), env=env)
+    return subprocess.call(launch_cmd(argv, nproc, _free_port(), script), env=env)
 
 
 def lib_sha256():
@@ -311,7 +312,11 @@ def main(argv=None):
         value = pr_per_step * steps / head["dt"]
         per_launch_pr = args.instances * args.n * args.rounds  # one GPU's launch
         inst_rounds = args.instances * args.rounds
-        alg_gbs = per_launch_pr * B_ALG_OTR / head["kernel_s"] / 1e9
+        # physical HBM bytes of one launch: the initial values read once (int32 per
+        # process), the results written once (decide value int32 + decide round u8 per process,
+        # a 24-B summary per instance); process state stays on chip for all R rounds
+        hbm_bytes = args.instances * (args.n * (4 + 4 + 1) + 24)
+        hbm_gbs = hbm_bytes / head["kernel_s"] / 1e9
         if devices:
             par = f"one context over devices {devices} (psg_config.devices), {args.instances} instances each"
         else:
@@ -352,11 +357,11 @@ def main(argv=None):
                 "traffic": None,
                 "kernel": "psg::otr_kernel<1, false, false, psg::NoHook, false>",  # <W, OTR2, explicit schedule, hook, trace>
                 "kernel_ms": head["kernel_s"] * 1e3,
-                "hbm_algorithmic": {
-                    "note": "SURVEY §8d accounting: 24 B of state per process-round as if streamed each "
-                            "round; a bookkeeping rate, not a physical bound",
-                    "bytes_per_process_round": B_ALG_OTR, "achieved": alg_gbs, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": alg_gbs / HBM_PEAK_GBS},
+                "hbm": {
+                    "model": "per launch: init values in (4 B/process) + decide values and rounds out "
+                             "(5 B/process) + instance summaries (24 B/instance); state stays in VGPRs",
+                    "bytes_per_launch": hbm_bytes, "achieved": hbm_gbs, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS},
             },
             "checks": {
                 "violations": psync.BatchResult(psync.OTR(), args.rounds, s).violations(),
@@ -399,6 +404,7 @@ def main(argv=None):
                 rl["traffic_unit"] = "GB/s"
                 rl["traffic_bytes_per_launch"] = d["hbm"]["traffic_bytes"]
                 rl["traffic_source"] = src + " (PMC FETCH_SIZE*2 + WRITE_SIZE per launch)"
+                rl["hbm"]["pmc_over_model"] = d["hbm"]["traffic_bytes"] / hbm_bytes
             else:
                 # counters of another build say nothing about this one's rates
                 rl["stale_profile"] = "profile taken on a different libpsg.so: achieved / frac / traffic " \

@@ -24,6 +24,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402  (first: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
+import bench  # noqa: E402  (plan / launch_ranks / dry_run: the same launch logic as the headline)
 from round_amd import abi  # noqa: E402
 from round_amd import dist as rdist  # noqa: E402
 from round_amd import psync  # noqa: E402
@@ -77,15 +78,34 @@ def configs(scale):
     return out
 
 
-def main():
+def parse(argv):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); > 1 without torchrun starts them as a child torchrun")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0, help="multiply the per-GPU instance counts")
     ap.add_argument("--only", default="", help="comma-separated name prefixes")
     ap.add_argument("--out", default="")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="set up the ranks (gloo) and print the plan without touching a GPU")
+    args = ap.parse_args(argv)
+    args.device_list = ""  # bench.plan's field: ranks only here
+    return args
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    # --gpus N really runs N ranks (bench.py's plan / launch logic), e.g. C3's
+    # 1e8 LastVoting instances over 8 GPUs and C5's all-reduced histogram from one command
+    mode, what = bench.plan(args, os.environ)
+    if mode == "device-list":
+        raise SystemExit("bench_configs.py runs ranks (--gpus N / torchrun), not device lists")
+    if mode == "launch":
+        sys.exit(bench.launch_ranks(argv, what, args.dry_run, script=__file__))
+    if args.dry_run:
+        return bench.dry_run(mode, what if mode == "ranks" else 1, int(os.environ.get("RANK", "0")), args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     dev = int(os.environ.get("LOCAL_RANK", "0"))
@@ -151,7 +171,8 @@ def main():
                 j += 2
         g.close()
         if rank == 0:
-            pr_launch = I * n * R
+            vb = 8 if alg.real else 4  # Double values for EpsilonConsensus
+            hbm_bytes = I * (n * (vb + vb + 1) + 24)
             th = [tot.term_hist[i] for i in range(R + 2)]
             done = sum(th[:-1])
             rec = {
@@ -159,11 +180,12 @@ def main():
                 "n_gpus": world,
                 "value": tot.process_rounds * args.steps / dt, "unit": "checked process-rounds/s",
                 "kernel_ms": kern * 1e3,
-                # SURVEY §8d bookkeeping: the state bytes of a process-round as if streamed from HBM
-                # every round (the kernels keep the state on chip; not a physical bound)
-                "hbm_algorithmic": {"bytes_per_process_round": balg,
-                                    "achieved": pr_launch * balg / kern / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                    "frac": pr_launch * balg / kern / 1e9 / HBM_PEAK_GBS},
+                # physical HBM bytes of one launch: initial values in, decide values /
+                # rounds and instance summaries out; state stays on chip for all R rounds
+                "hbm": {"bytes_per_launch": hbm_bytes, "achieved": hbm_bytes / kern / 1e9, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": hbm_bytes / kern / 1e9 / HBM_PEAK_GBS},
+                # SURVEY §8d's state bytes per process-round as if streamed every round (bookkeeping)
+                "alg_bytes_per_process_round": balg,
                 "process_rounds_active": tot.active_process_rounds,
                 "instance_rounds_live": tot.live_instance_rounds,
                 "violations": psync.BatchResult(alg, R, tot).violations(),

@@ -419,6 +419,13 @@ const char* psg_create_error(void);
  * empty set. */
 int psg_selftest_map_head(int32_t device, const uint64_t* sets, int32_t count, int32_t tiebreak, int32_t* out_first);
 
+/* Self-test hook (tests only): runs `n_ops` (opcode, pos) pairs on one W-word HO mask
+ * (Mask<W>, W = 1..4) on device `device`, the device analogue of psync.utils.LongBitSet
+ * (LongBitSet.scala:5-33: a 64-bit set whose index is taken mod 64; W words: mod 64W).
+ * Opcodes: 0 empty, 1 full, 2 set(pos), 3 clear(pos), 4 flip(pos), 5 get(pos) -> out,
+ * 6 size -> out. Results of get / size are written to out[0..n_out) in order. */
+int psg_selftest_bitset(int32_t device, int32_t W, const int32_t* ops, int32_t n_ops, int32_t* out, int32_t n_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -600,6 +600,25 @@ struct Callback { /* ConsensusIO.decide / RealConsensusIO.decide */
 template <class A>
 struct Msg { int src; A payload; };
 
+
+/* Otr2.scala:32-36, the `ensuring` clause of mmor, literally:
+ *   mailbox.forall{ case (k, v2) =>
+ *     mailbox.count{ case (k, v3) => v1 == v3 } > mailbox.count{ case (k, v3) => v2 == v3 } || v1 <= v2 }
+ * evaluated on every mmor the oracle executes (OTR and OTR2 share the round); the counters
+ * are read by tests/test_reference_pins.py through oracle_mmor_ensuring_stats. */
+static std::atomic<uint64_t> g_mmor_calls{0}, g_mmor_ensuring_failures{0};
+static void mmor_ensuring(const std::vector<Msg<int32_t>>& mb, int32_t v1) {
+  auto count = [&](int32_t v) {
+    int c = 0;
+    for (auto& m : mb) c += m.payload == v;
+    return c;
+  };
+  bool ok = true;
+  for (auto& m : mb) ok = ok && (count(v1) > count(m.payload) || v1 <= m.payload);
+  g_mmor_calls.fetch_add(1, std::memory_order_relaxed);
+  if (!ok) g_mmor_ensuring_failures.fetch_add(1, std::memory_order_relaxed);
+}
+
 /* ---------------- OTR: example/Otr.scala:13-86 ---------------- */
 struct Otr {
   struct P {
@@ -617,16 +636,21 @@ struct Otr {
   /* send(): broadcast(x) */
   bool sends_to(const P&, int, int, int) const { return true; }
   Payload payload(const P& s, int, int, int) const { return s.x; }
-  /* mmor, Otr.scala:44-49: groupBy value, minBy (-size, v) */
-  static int32_t mmor(const std::vector<Msg<int32_t>>& mb) {
+  /* mmor, Otr.scala:44-49: groupBy value, minBy (-size, v). Every result is checked against
+   * the post-condition the reference states for the same function (Otr2.scala:32-36):
+   * mailbox.forall{ (k, v2) => count(v1) > count(v2) || v1 <= v2 } (mmor_ensuring below). */
+  int32_t mmor(const std::vector<Msg<int32_t>>& mb) const {
     std::map<int32_t, int> byValue;
     for (auto& m : mb) byValue[m.payload]++;
     bool first = true;
     std::pair<int, int32_t> best{0, 0};
     for (auto& kv : byValue) {
-      std::pair<int, int32_t> key{-kv.second, kv.first};
+      /* variant 2 (oracle-only mutant, tests): ties go to the LARGER value */
+      std::pair<int, int32_t> key{-kv.second, variant == 2 ? -kv.first : kv.first};
       if (first || key < best) { best = key; first = false; }
     }
+    if (variant == 2) best.second = -best.second;
+    mmor_ensuring(mb, best.second);
     return best.second;
   }
   /* update, Otr.scala:63-81; returns true on exitAtEndOfRound */
@@ -1627,6 +1651,16 @@ static thread_local std::string g_oracle_err;
 const char* oracle_last_error(void) { return g_oracle_err.c_str(); }
 
 void oracle_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) { orc::philox4x32_10(ctr, key, out); }
+
+/* mmor calls and violations of Otr2.scala:32-36's ensuring clause since the last reset */
+void oracle_mmor_ensuring_stats(uint64_t* calls, uint64_t* failures, int32_t reset) {
+  if (calls) *calls = orc::g_mmor_calls.load();
+  if (failures) *failures = orc::g_mmor_ensuring_failures.load();
+  if (reset) {
+    orc::g_mmor_calls = 0;
+    orc::g_mmor_ensuring_failures = 0;
+  }
+}
 
 int oracle_java_first_boolean(int64_t seed) { return orc::java_random_first_boolean((uint64_t)seed) ? 1 : 0; }
 

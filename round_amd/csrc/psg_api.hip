@@ -272,6 +272,30 @@ static int run_kernel(psg_ctx* c, KArgs& a, uint64_t count, psg_summary* out, bo
   return PSG_OK;
 }
 
+// psg_selftest_bitset: LongBitSet's operations (LongBitSet.scala:7-23) on Mask<W>, one lane
+template <int W>
+__global__ void bitset_selftest_kernel(const int32_t* ops, int n_ops, int32_t* out, int n_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Mask<W> m = mzero<W>();
+  int o = 0;
+  for (int i = 0; i < n_ops; ++i) {
+    const int op = ops[2 * i], pos = ops[2 * i + 1] & (64 * W - 1);  // index mod 64 (mod 64W)
+    switch (op) {
+      case 0: m = mzero<W>(); break;
+      case 1: m = mfull<W>(64 * W); break;
+      case 2: mset(m, pos); break;
+      case 3: mclear(m, pos); break;
+      case 4:
+        if (mtest(m, pos)) mclear(m, pos);
+        else mset(m, pos);
+        break;
+      case 5: if (o < n_out) out[o++] = mtest(m, pos) ? 1 : 0; break;
+      case 6: if (o < n_out) out[o++] = mpopc(m); break;
+      default: break;
+    }
+  }
+}
+
 extern "C" {
 
 int psg_config_default(psg_config* cfg, int32_t alg, int32_t n) {
@@ -401,6 +425,36 @@ int psg_selftest_map_head(int32_t device, const uint64_t* sets, int32_t count, i
     rc = PSG_EIO;
   }
   if (d_sets) (void)hipFree(d_sets);
+  if (d_out) (void)hipFree(d_out);
+  return rc;
+}
+
+int psg_selftest_bitset(int32_t device, int32_t W, const int32_t* ops, int32_t n_ops, int32_t* out, int32_t n_out) {
+  if (!ops || !out || n_ops < 0 || n_out < 0 || W < 1 || W > 4) return PSG_EINVAL;
+  if (n_ops == 0) return PSG_OK;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return PSG_ENODEV;
+  if (hipSetDevice(device) != hipSuccess) return PSG_ENODEV;
+  int32_t *d_ops = nullptr, *d_out = nullptr;
+  int rc = PSG_OK;
+  const size_t ob = sizeof(int32_t) * (n_out > 0 ? n_out : 1);
+  if (hipMalloc(&d_ops, sizeof(int32_t) * 2 * (size_t)n_ops) != hipSuccess || hipMalloc(&d_out, ob) != hipSuccess) {
+    rc = PSG_ENOMEM;
+  } else if (hipMemcpy(d_ops, ops, sizeof(int32_t) * 2 * (size_t)n_ops, hipMemcpyHostToDevice) != hipSuccess ||
+             hipMemset(d_out, 0xFF, ob) != hipSuccess) {
+    rc = PSG_EIO;
+  } else {
+    switch (W) {
+      case 1: hipLaunchKernelGGL(bitset_selftest_kernel<1>, dim3(1), dim3(64), 0, nullptr, d_ops, n_ops, d_out, n_out); break;
+      case 2: hipLaunchKernelGGL(bitset_selftest_kernel<2>, dim3(1), dim3(64), 0, nullptr, d_ops, n_ops, d_out, n_out); break;
+      case 3: hipLaunchKernelGGL(bitset_selftest_kernel<3>, dim3(1), dim3(64), 0, nullptr, d_ops, n_ops, d_out, n_out); break;
+      default: hipLaunchKernelGGL(bitset_selftest_kernel<4>, dim3(1), dim3(64), 0, nullptr, d_ops, n_ops, d_out, n_out); break;
+    }
+    if (hipGetLastError() != hipSuccess ||
+        (n_out > 0 && hipMemcpy(out, d_out, sizeof(int32_t) * n_out, hipMemcpyDeviceToHost) != hipSuccess))
+      rc = PSG_EIO;
+  }
+  if (d_ops) (void)hipFree(d_ops);
   if (d_out) (void)hipFree(d_out);
   return rc;
 }

@@ -25,7 +25,7 @@ EXPORTED_SYMBOLS = [
     "psg_selftest_map_head", "psg_load_inputs_f64", "psg_copy_decisions_f64", "psg_fetch_instances_f64",
     "psg_run_batch_spec", "psg_load_schedule", "psg_clear_schedule", "psg_materialize_schedule",
     "psg_population_fresh", "psg_population_next", "psg_population_read", "psg_spec_from_text", "psg_spec_release",
-    "psg_spec_compile_native", "psg_spec_native_source",
+    "psg_spec_compile_native", "psg_spec_native_source", "psg_selftest_bitset",
 ]
 
 
@@ -91,6 +91,8 @@ def load():
     L.psg_spec_release.restype = None
     L.psg_selftest_map_head.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
                                         C.POINTER(C.c_int32)]
+    L.psg_selftest_bitset.argtypes = [C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.c_int32,
+                                      C.POINTER(C.c_int32), C.c_int32]
     _lib = L
     return L
 
@@ -325,6 +327,26 @@ def selftest_map_head(sets, tiebreak=abi.PSG_TIE_CHAMP, device=0):
     if rc != 0:
         raise PsgError(rc, "psg_selftest_map_head failed")
     return list(out)[:k]
+
+
+BITSET_OPS = {"empty": 0, "full": 1, "set": 2, "clear": 3, "flip": 4, "get": 5, "size": 6}
+
+
+def selftest_bitset(ops, W=1, device=0):
+    """Run [(op, pos)] (BITSET_OPS names) on one Mask<W> on the GPU; the get / size results
+    in order (test hook: psync.utils.LongBitSet's operations on the device HO word)."""
+    L = load()
+    flat = []
+    n_out = 0
+    for op, pos in ops:
+        flat += [BITSET_OPS[op], int(pos)]
+        n_out += op in ("get", "size")
+    arr = (C.c_int32 * max(1, len(flat)))(*flat)
+    out = (C.c_int32 * max(1, n_out))()
+    rc = L.psg_selftest_bitset(device, W, arr, len(ops), out, n_out)
+    if rc != 0:
+        raise PsgError(rc, "psg_selftest_bitset failed")
+    return list(out)[:n_out]
 
 
 def spec_from_text(text, alg=0):

@@ -74,3 +74,13 @@ def test_host_cores_respects_quota(monkeypatch):
     assert bench.host_cores() == (16, 256, 16.0)
     monkeypatch.setattr(bench, "_cpu_quota", lambda: None)
     assert bench.host_cores()[0] == 256
+
+
+def test_bench_configs_gpus_two_spawns_two_ranks():
+    """VERDICT r3 #10: bench_configs.py --gpus N runs N ranks from one command (C3 over 8 GPUs)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench_configs.py"), "--gpus", "2", "--dry-run",
+                        "--only", "C3"], cwd=ROOT, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    assert json.loads(lines[0]) == {"dry_run": True, "mode": "ranks", "world": 2, "ranks_seen": 2, "n_gpus": 2}
