@@ -253,7 +253,18 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
       uint32_t cls = 0xFFFFu;
       Mask<W> rem = act, D = mzero<W>();
       bool cols = false;
+      // Every alive sender holding the same t (the common case once round 0 has spread the
+      // origins: D is empty) is one compare per slot against the first alive sender's t and
+      // a ballot, instead of the wave AND / OR reductions that find I and U (C4 f = 64 8.53 ->
+      // 8.0 ms, f = 1 2.17 -> 2.08 ms)
       if (!closed) {
+        const Mask<W> t0 = load_t<W, 64 * W>(L.ts, mfirst(act));
+        uint32_t dif = 0;
+#pragma unroll
+        for (int j = 0; j < W; ++j) dif |= (uint32_t)((act.w[j] >> P.lane) & 1ull) & (meq(t[j], t0) ? 0u : 1u);
+        cols = !pk_any(dif);  // D is empty: the column form with no column
+      }
+      if (!closed && !cols) {
         Mask<W> il, ul;
 #pragma unroll
         for (int w = 0; w < W; ++w) {

@@ -172,12 +172,17 @@ PSG_DEV void otr_body(const KArgs& a) {
     pt.mark(0);
 
     int32_t live_rounds = 0;  // rounds in which some process took a step
+    int kf = a.R;             // first round in which every process had halted (the state is final)
     for (int k = 0; k < a.R; ++k) {
       const uint32_t old01 = dec01;
       const int32_t old_decision = decision;
       const Mask<W> act = g.ballot_any(halted01 == 0u);  // lanes past n are halted
       int32_t hs = n;  // |mailbox| of this round (Spec field HOSIZE)
-      if (many(act)) {
+      if (!many(act)) {  // every process halted: the frozen tail below (25.3 -> 24.8 ms)
+        kf = k;
+        break;
+      }
+      {
         live_rounds = k + 1;
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
@@ -259,7 +264,16 @@ PSG_DEV void otr_body(const KArgs& a) {
       if constexpr (!SH::kFused)
         otr_check<W, V2>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, old01, old_decision, valid01, od, ox);
       if (tracing_on) trace(k + 1, hs);
-      pt.mark(many(act) ? 1 : 2);
+      pt.mark(1);
+    }
+    // Rounds kf .. R-1: every process has halted, so no process takes a step and the state, the
+    // pre-round (old) state included, is the final one; the Spec is still evaluated at each of
+    // these check points, kf + 1 .. R (Otr.scala:95-120 over the frozen state).
+    for (int k = kf; k < a.R; ++k) {
+      if constexpr (!SH::kFused)
+        otr_check<W, V2>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, dec01, decision, valid01, od, ox);
+      if (tracing_on) trace(k + 1, n);
+      pt.mark(2);
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 8, dec_val, dec_round, halt_round, x, &bc,
                        &tally, live_rounds);

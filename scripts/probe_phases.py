@@ -21,7 +21,7 @@ elif which == "fm":
 elif which == "kset4":  # the C4 KSet rows' schedule (bench_configs.py)
     runs = [(psync.KSetAgreement(2), 256, 16, 200_000,
              dict(schedule=psync.HOSchedule(drop_log2=0, good_round=0.0, crash_fmax=f)), f"KSet C4 f={f}")
-            for f in (1, 32)]
+            for f in (0, 1, 32, 64)]
 else:
     runs = [(psync.KSetAgreement(2), 256, 16, 200_000, {}, "KSet k=2")]
 for alg, n, R, I, kw, label in runs:

@@ -34,6 +34,7 @@ for spec in args.kernel:
         nth = int(k)
     v = [float(x) for x in nums.split(",")]
     kernels.append((name, v[0], int(v[1]), int(v[2]), v[3] if len(v) > 3 else None, nth))
+label = {id(k): k[0] + ("" if k[5] is None else f"#{k[5]}") for k in kernels}  # one entry per spec
 
 os.makedirs(args.dst, exist_ok=True)
 stats = os.path.join(args.src, "kt", "run_kernel_stats.csv")
@@ -43,9 +44,24 @@ if os.path.exists(stats):
     for r in csv.DictReader(open(stats)):
         for k in kernels:
             if k[0] in r["Name"] and k[5] is None:
-                avg_ns[k[0]] = float(r["AverageNs"])
+                avg_ns[label[id(k)]] = float(r["AverageNs"])
 
-per = {k[0]: collections.defaultdict(list) for k in kernels}
+# the nth dispatch of a kernel (name#k) is timed from the kernel-trace pass's own per-dispatch
+# records (the same command, so the same dispatch sequence), never from the PMC passes'
+# timestamps: counter collection stretches a dispatch (c10_pmc's KSet entry read 2.77 GHz)
+trace = os.path.join(args.src, "kt", "run_kernel_trace.csv")
+if os.path.exists(trace):
+    rows = list(csv.DictReader(open(trace)))
+    for k in kernels:
+        if k[5] is None:
+            continue
+        ds = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if k[0] in r["Kernel_Name"]]
+        if k[5] < len(ds):
+            avg_ns[label[id(k)]] = float(ds[k[5]])
+
+MAX_CLOCK_GHZ = 2.4  # MI355X peak engine clock: a derived clock above it means a wrong duration
+
+per = {label[id(k)]: collections.defaultdict(list) for k in kernels}
 meta = {}
 for d in sorted(os.listdir(args.src)):
     f = os.path.join(args.src, d, "run_counter_collection.csv")
@@ -58,25 +74,31 @@ for d in sorted(os.listdir(args.src)):
                 continue
             by_dispatch[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
             by_dispatch[r["Dispatch_Id"]]["_dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-            meta[k[0]] = {x: r[x] for x in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
+            meta[label[id(k)]] = {x: r[x] for x in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
                                             "Scratch_Size", "VGPR_Count", "SGPR_Count")}
         disp = [by_dispatch[d] for d in sorted(by_dispatch, key=int)]
         if k[5] is not None:
             disp = disp[k[5]:k[5] + 1]
         for vals in disp:
             for c, v in vals.items():
-                per[k[0]][c].append(v)
+                per[label[id(k)]][c].append(v)
 
 out = {}
-for name, inst, R, n, bpr, _ in kernels:
+for k in kernels:
+    _, inst, R, n, bpr, _ = k
+    name = label[id(k)]
     avg = {c: sum(v) / len(v) for c, v in per[name].items()}
-    ns = avg_ns.get(name) or avg.get("_dur_ns")
+    ns = avg_ns.get(name)  # kernel-trace duration only (None: no rates)
     W = (n + 63) // 64
     inst_rounds = inst * R
     o = {"dispatch": meta.get(name), "kernel_trace_avg_ns": avg_ns.get(name),
          "workload": {"instances": inst, "rounds": R, "n": n, "waves_per_instance": W,
                       "process_rounds": inst * R * n},
          "pmc_per_launch": {c: v for c, v in avg.items() if not c.startswith("_")}}
+    if ns and "GRBM_GUI_ACTIVE" in avg and avg["GRBM_GUI_ACTIVE"] / 8 / ns > MAX_CLOCK_GHZ * 1.02:
+        o["clock_error"] = (f"GRBM_GUI_ACTIVE / 8 / trace duration = {avg['GRBM_GUI_ACTIVE'] / 8 / ns:.2f} GHz "
+                            f"> {MAX_CLOCK_GHZ} GHz: the duration does not belong to these counters; no rates")
+        ns = None
     if ns and "GRBM_GUI_ACTIVE" in avg:
         cyc = avg["GRBM_GUI_ACTIVE"] / 8
         o["clock_GHz"] = cyc / ns
