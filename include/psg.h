@@ -330,6 +330,13 @@ void psg_spec_release(psg_spec_program* prog);
  * override). No device needed to compile. */
 int psg_spec_compile_native(const char* text, int32_t alg, int32_t fused, int32_t n, const char* cache_dir,
                             psg_spec_program* out, char* names, size_t names_len, char* err, size_t err_len);
+/* The Spec of Formula text after the native lowering's exact V.exists / quantifier rewrites
+ * (hoisted conjuncts free of a bound variable, split foralls), as Formula text — invariants
+ * already guarded by their round invariants, (phase 1) — so the rewrites can be checked
+ * against the Spec as written under any evaluator (tests). Same buffer contract as
+ * psg_spec_native_source. PSG_SPEC_OPTIONS (environment, comma-separated) holds generator
+ * options for all three entry points: nosym, nosplit, D<NAME>=<VALUE>. */
+int psg_spec_rewrite_text(const char* text, int32_t alg, char* out, size_t* out_len, char* err, size_t err_len);
 /* The HIP source psg_spec_compile_native compiles for these arguments (tests, inspection):
  * *src_len = capacity in, the size needed (with the terminating NUL) out; PSG_ERANGE when
  * src is NULL or too small. */

@@ -1,16 +1,15 @@
 // psg_spec_gen.cpp — psg_spec_compile_native: a Spec given as Formula text lowered to native
-// gfx950 code in-process, the C-ABI (and so the JVM, integration/scala/GpuSpec.scala) route to
-// the native and fused Spec modules that round_amd/formula.py compile_native builds from
-// Python. The generator is the same as formula.py's codegen_hip / _fused_source (the HIP
-// source is byte-for-byte the one Python writes for the same text,
-// tests/test_spec_native_text.py), the code object is compiled with hiprtc (no process is
-// started) and cached under the same key as Python's (sha256 of the source and the kernel
-// headers), so either route reuses the other's module. Host C++ only.
+// gfx950 code in-process. It is the only Spec generator: the C ABI (and so the JVM,
+// integration/scala/GpuSpec.scala) calls it directly, round_amd/formula.py compile_native
+// writes a DSL Spec as Formula text and calls it. The code object is compiled with hiprtc (no
+// process is started) and cached by a hash of the toolchain, the source and the kernel
+// headers. Host C++ only.
 //
 // Reference: the Spec being lowered is a psync.Spec (psync/Specs.scala:8-16) whose Formula
 // trees (psync/formula/Formula.scala:5-585) arrive as text; the rewrites below are exact
-// for every input (formula.py: equality pins, count guards, breakpoint finitization,
-// tuple quantifiers, memoized init membership, common closed subformulas).
+// for every input (equality pins, count guards, breakpoint finitization, tuple quantifiers,
+// memoized init membership, common closed subformulas, split foralls; DESIGN.md §5;
+// psg_spec_rewrite_text exposes the tree rewrites to the tests).
 #include <hip/hiprtc.h>
 
 #include <algorithm>
@@ -33,8 +32,34 @@
 namespace psgspec {
 namespace {
 
-// ------------------------------------------------------------------ tree helpers (= formula.py)
+// ------------------------------------------------------------------ tree helpers
 bool is_var(const Tree& T, int e, int uid) { return T.nodes[e].k == VAR && T.nodes[e].uid == uid; }
+
+// Generator options (experiments and profiling builds), from the environment variable
+// PSG_SPEC_OPTIONS, comma-separated: "nosym" (no symmetric-check-point lowering), "nosplit"
+// (no split foralls / hoisted conjuncts), "D<NAME>=<VALUE>" (a #define at the top of the
+// module, e.g. DPSG_PHASE_TIMERS=1). They change the source, hence the cache key.
+struct GenOptions {
+  bool symmetric = true, split = true;
+  std::vector<std::string> defines;
+};
+GenOptions g_opts;  // set by load_options() before each generation (the entry points)
+void load_options() {
+  g_opts = GenOptions{};
+  const char* e = std::getenv("PSG_SPEC_OPTIONS");
+  std::string t = e ? e : "";
+  size_t i = 0;
+  while (i <= t.size()) {
+    const size_t j = t.find(',', i);
+    const std::string tok = t.substr(i, j == std::string::npos ? std::string::npos : j - i);
+    if (tok == "nosym") g_opts.symmetric = false;
+    else if (tok == "nosplit") g_opts.split = false;
+    else if (tok.size() > 1 && tok[0] == 'D') g_opts.defines.push_back(tok.substr(1));
+    else if (!tok.empty()) throw SpecError("PSG_SPEC_OPTIONS: unknown option " + tok);
+    if (j == std::string::npos) break;
+    i = j + 1;
+  }
+}
 
 // Python's `is` on the trees formula.py from_text builds: a variable is one object per binder
 bool same_obj(const Tree& T, int a, int b) {
@@ -91,7 +116,7 @@ std::pair<int, int> init_member(const Tree& T, int q) {
 }
 
 // Fields (field, tag) through which the body reads the quantified process, or false if the
-// variable is used otherwise (formula.py _tuple_fields)
+// variable is used otherwise
 bool tuple_fields(const Tree& T, int q, std::vector<std::pair<int, int>>& out) {
   const Node& Q = T.nodes[q];
   std::vector<int> w;
@@ -110,7 +135,7 @@ bool tuple_fields(const Tree& T, int q, std::vector<std::pair<int, int>>& out) {
   return out.size() <= 4;
 }
 
-// Structural key of node e, bound variables numbered by binding depth from e (formula.py _skey):
+// Structural key of node e, bound variables numbered by binding depth from e:
 // two closed subformulas with equal keys are the same formula.
 std::string skey_rec(const Tree& T, int e, std::map<int, int>& env) {
   const Node& n = T.nodes[e];
@@ -132,7 +157,7 @@ std::string skey_rec(const Tree& T, int e, std::map<int, int>& env) {
       const std::string pre = n.k == QUANT ? "Q(" + std::to_string(n.qk) + "," : "C(" + skey_rec(T, n.a, env) + ",";
       const bool had = env.count(n.uid) > 0;
       const int old = had ? env[n.uid] : 0;
-      const int level = (int)env.size();  // formula.py: {**env, uid: len(env)}
+      const int level = (int)env.size();  // binding depth
       env[n.uid] = level;
       const std::string body = skey_rec(T, n.k == QUANT ? n.a : n.b, env);
       if (had) env[n.uid] = old;
@@ -144,7 +169,7 @@ std::string skey_rec(const Tree& T, int e, std::map<int, int>& env) {
 }
 
 // Does the body of process quantifier q read its variable only through current / old fields
-// (no init field, no use as a pid)? (formula.py _symmetric)
+// (no init field, no use as a pid)?
 bool symmetric(const Tree& T, int q) {
   const int uid = T.nodes[q].uid;
   std::vector<int> w;
@@ -163,7 +188,7 @@ bool symmetric(const Tree& T, int q) {
 }
 
 // Conjuncts A of forall(j => A && .. ==> B) / exists, count(j => A && .. && B) that read only j
-// (formula.py _tuple_guard): the processes where one fails contribute nothing
+//: the processes where one fails contribute nothing
 std::vector<int> tuple_guard(const Tree& T, int q) {
   const Node& Q = T.nodes[q];
   std::vector<int> cs, out;
@@ -256,7 +281,7 @@ bool intersects(const std::set<int>& a, const std::set<int>& b) {
   return false;
 }
 
-// Equality pins of the V.exists variable uid in body (formula.py _pins)
+// Equality pins of the V.exists variable uid in body
 bool pins(const Tree& T, int body, int uid, const std::set<int>& banned, Pins& out) {
   std::vector<int> cs;
   conjuncts(T, body, cs);
@@ -353,7 +378,7 @@ bool count_guard(const Tree& T, int q, CountGuard& g) {
 }
 
 // e reads a field of a process other than uid, or holds a quantifier / set membership
-// (formula.py _cross)
+//
 bool cross(const Tree& T, int e, int uid) {
   std::vector<int> w;
   T.walk(e, w);
@@ -367,18 +392,17 @@ bool cross(const Tree& T, int e, int uid) {
 
 // V.exists(v => A && B(v)) -> A && V.exists(v => B(v)) for the conjuncts A free of v, a conjunct
 // P.forall(i => A && B) split into P.forall(A) && P.forall(B) first, A the conjuncts free of v
-// doing cross-lane work (formula.py _rewrite_vint / _split_forall / _vint_step, shared
-// subformulas stay shared)
+// doing cross-lane work (shared subformulas stay shared)
 // the conjuncts of quantifier q's body, each P.forall(i => A && B) among them split into
 // P.forall(A), P.forall(B): A the conjuncts free of q's variable (and doing cross-lane work,
-// cross_only) (formula.py _split_forall)
+// cross_only)
 void split_conjuncts(Tree& T, int q, bool cross_only, std::vector<int>& cs) {
   const int uid = T.nodes[q].uid;
   std::vector<int> cs0;
   conjuncts(T, T.nodes[q].a, cs0);
   for (int c : cs0) {
     const Node C = T.nodes[c];
-    if (C.k == QUANT && C.qk == QFORALL) {
+    if (g_opts.split && C.k == QUANT && C.qk == QFORALL) {
       std::vector<int> ds, dfr, dbd;
       conjuncts(T, C.a, ds);
       for (int d : ds) (!free_of(T, d).count(uid) && (!cross_only || cross(T, d, C.uid)) ? dfr : dbd).push_back(d);
@@ -395,8 +419,9 @@ void split_conjuncts(Tree& T, int q, bool cross_only, std::vector<int>& cs) {
 }
 
 // P.exists(j => A && B(j)) -> A && P.exists(j => B(j)), the same for P.forall (n >= 1), for the
-// conjuncts A free of j (formula.py _proc_step)
+// conjuncts A free of j
 int proc_step(Tree& T, int q) {
+  if (!g_opts.split) return q;
   const int uid = T.nodes[q].uid, qk = T.nodes[q].qk;
   std::vector<int> cs, fr, bd;
   split_conjuncts(T, q, false, cs);
@@ -459,7 +484,7 @@ std::string S(int v) { return std::to_string(v); }
 
 using Code = std::pair<std::string, bool>;  // (C++ expression, depends on the lane)
 
-// ------------------------------------------------------------------ the generator (= formula.py _Gen)
+// ------------------------------------------------------------------ the generator
 struct Gen {
   Tree& T;
   bool restrict_fields;
@@ -482,7 +507,7 @@ struct Gen {
     std::map<int, int> env;
     return skeys[e] = skey_rec(T, e, env);
   }
-  // (field tuple, guard code or "") -> TupU / TupG name (formula.py tup_sets)
+  // (field tuple, guard code or "") -> TupU / TupG name
   using TupKey = std::pair<std::vector<std::pair<int, int>>, std::string>;
   std::vector<std::pair<TupKey, std::string>> tup_sets;
   std::set<TupKey> tup_used;
@@ -743,7 +768,7 @@ struct Gen {
     return vint_unpinned(q, v, in_lane, vi);
   }
 
-  // A process quantifier on a symmetric check point (formula.py _quant_uni), false for the
+  // A process quantifier on a symmetric check point, false for the
   // general rules: a body reading its variable only through current / old fields has one value
   // for every process; P.exists(j => init(j.f) == t) with a group-uniform t is a scalar-memoized probe
   bool quant_uni(int q, const std::string& v, bool in_lane, int vi, Code& out) {
@@ -866,7 +891,7 @@ struct Gen {
   }
 };
 
-// The native checker's source (= formula.py codegen_hip) for a parsed + compiled Spec.
+// The native checker's source for a parsed + compiled Spec.
 std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
   Tree& T = P.T;
   Gen gen{T, alg != 0, alg != 0 ? alg_fields(alg) : std::set<int>{}};
@@ -918,7 +943,7 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
     int slot = 0;
   };
   // the slot lines of fail() and the Termination expression, under the general or the
-  // symmetric-check-point lowering (formula.py codegen_hip block)
+  // symmetric-check-point lowering
   auto block = [&](bool uni) {
     gen.uni = uni;
     gen.cse.clear();
@@ -999,8 +1024,8 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
   const bool has_term = G.has_term && !G.term.empty();
   const std::string term = G.term;
   std::vector<std::string> body, term_decls;
-  // worth its test only with few fields to compare (formula.py SYMMETRIC_MAX_FIELDS)
-  if (!gen.uft.empty() && gen.uft.size() <= 6) {
+  // worth its test only with few fields to compare
+  if (g_opts.symmetric && !gen.uft.empty() && gen.uft.size() <= 6) {
     uint32_t cur = 0, old = 0;
     for (auto& ft : gen.uft) {
       if (ft.second == PSG_TAG_CUR) cur |= 1u << ft.first;
@@ -1026,7 +1051,7 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
   for (int f : gen.fields) fmask |= 1u << f;
   for (int t : gen.tags) tmask |= 1u << t;
   std::ostringstream o;
-  o << "// generated by round_amd/formula.py (codegen_hip): native checker of one Spec\n"
+  o << "// generated by psg_spec_gen.cpp: native checker of one Spec\n"
     << "#include \"psg_spec_native.hpp\"\n"
     << "namespace psg {\n"
     << "struct GenSpec {\n"
@@ -1057,7 +1082,7 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
   return o.str();
 }
 
-// algorithm -> (round-kernel source, body template, leading template arguments) (formula.py FUSED_KERNELS)
+// algorithm -> (round-kernel source, body template, leading template arguments)
 bool fused_kernel(int alg, std::string& src, std::string& body, std::string& targs_w_prefix, std::string& targs_tail) {
   targs_tail.clear();
   switch (alg) {
@@ -1075,7 +1100,7 @@ bool fused_kernel(int alg, std::string& src, std::string& body, std::string& tar
   return true;
 }
 
-// The algorithm's round kernel instantiated with the generated Spec as its hook (formula.py _fused_source)
+// The algorithm's round kernel instantiated with the generated Spec as its hook
 std::string fused_source(int alg, const std::vector<int>& waves) {
   std::string src, body, pre, tail;
   if (!fused_kernel(alg, src, body, pre, tail)) throw SpecError("fused lowering needs one of the integer-state algorithms");
@@ -1188,6 +1213,12 @@ std::string env_or(const char* name, const std::string& dflt) {
 // The full module source of compile_native(text, alg, fused, n) and its cache key.
 std::string module_source(ParsedSpec& P, const Compiled& prog, int alg, bool fused, int n) {
   std::string src = codegen_hip(P, prog, alg);
+  std::string defs;
+  for (const std::string& d : g_opts.defines) {
+    const size_t eq = d.find('=');
+    defs += "#define " + (eq == std::string::npos ? d : d.substr(0, eq) + " " + d.substr(eq + 1)) + "\n";
+  }
+  src = defs + src;
   if (fused) {
     std::vector<int> waves;
     if (n > 0) waves.push_back((n + 63) / 64);
@@ -1195,6 +1226,45 @@ std::string module_source(ParsedSpec& P, const Compiled& prog, int alg, bool fus
     src = "#define PSG_FUSED_MODULE 1\n" + src + fused_source(alg, waves);
   }
   return src;
+}
+
+// A tree as Formula text (the format psg_spec_from_text reads; formula.py to_text)
+std::string text_of(const Tree& T, int e) {
+  static const char* fields[] = {"x", "decided", "decision", "ts", "ready", "commit", "vote", "canDecide"};
+  static const std::map<int, const char*> bins = {
+      {PSG_OP_AND, "And"}, {PSG_OP_OR, "Or"},     {PSG_OP_IMPL, "Implies"}, {PSG_OP_EQ, "Eq"},
+      {PSG_OP_NE, "Neq"},  {PSG_OP_LT, "Lt"},     {PSG_OP_LE, "Leq"},       {PSG_OP_GT, "Gt"},
+      {PSG_OP_GE, "Geq"},  {PSG_OP_ADD, "Plus"},  {PSG_OP_SUB, "Minus"},    {PSG_OP_MUL, "Times"},
+      {PSG_OP_DIV, "Divides"}, {PSG_OP_MOD, "Remainder"}};
+  const Node& n = T.nodes[e];
+  auto var = [](int uid) { return "v" + S(uid); };
+  switch (n.k) {
+    case LIT: return "(Lit " + S(n.v) + ")";
+    case NV: return "(Var n)";
+    case RV: return "(Var r)";
+    case COORDV: return "(Var coord)";
+    case VAR: return "(Var " + var(n.uid) + ")";
+    case FIELD: {
+      if (n.f == PSG_FIELD_HOSIZE) return "(App Cardinality (App HO " + text_of(T, n.a) + "))";
+      const std::string pre = n.tag == PSG_TAG_OLD ? "__old__" : n.tag == PSG_TAG_INIT ? "__init__" : "";
+      return "(App " + pre + fields[n.f] + " " + text_of(T, n.a) + ")";
+    }
+    case UN:
+      return std::string("(App ") + (n.op == PSG_OP_NOT ? "Not" : n.op == PSG_OP_NEG ? "Minus" : "IsDefined") + " " +
+             text_of(T, n.a) + ")";
+    case BIN: return std::string("(App ") + bins.at(n.op) + " " + text_of(T, n.a) + " " + text_of(T, n.b) + ")";
+    case CONTAINS:
+      return "(App In " + text_of(T, n.a) + " (Comprehension ((" + var(n.uid) + " pid)) " + text_of(T, n.b) + "))";
+    case QUANT:
+      switch (n.qk) {
+        case QFORALL: return "(ForAll ((" + var(n.uid) + " pid)) " + text_of(T, n.a) + ")";
+        case QEXISTS: return "(Exists ((" + var(n.uid) + " pid)) " + text_of(T, n.a) + ")";
+        case QCOUNT: return "(App Cardinality (Comprehension ((" + var(n.uid) + " pid)) " + text_of(T, n.a) + "))";
+        case QVINT: return "(Exists ((" + var(n.uid) + " Int)) " + text_of(T, n.a) + ")";
+        default: return "(Exists ((" + var(n.uid) + " Bool)) " + text_of(T, n.a) + ")";
+      }
+  }
+  throw SpecError("text_of: unknown node");
 }
 
 std::mutex g_paths_mu;
@@ -1216,7 +1286,13 @@ int compile_module(const std::string& src, int alg, bool fused, const char* cach
     hdr_names.push_back("psg_kernels.hpp");
     hdr_names.push_back("psg_packed.hpp");
   }
+  // the cache key: the source, the kernel headers and psg.h, and the compiler's identity
+  // (hiprtc version and options), so a module built by another toolchain is never reused
+  int rtc_major = 0, rtc_minor = 0;
+  (void)hiprtcVersion(&rtc_major, &rtc_minor);
+  const std::string toolchain = "hiprtc " + S(rtc_major) + "." + S(rtc_minor) + " --offload-arch=gfx950 -O3 -std=c++17";
   Sha256 h;
+  h.update(toolchain);
   h.update(src);
   for (auto& nm : hdr_names) {
     std::string t;
@@ -1234,7 +1310,7 @@ int compile_module(const std::string& src, int alg, bool fused, const char* cach
   h.update(psgh);
   const std::string dir = cache_dir && *cache_dir ? std::string(cache_dir) : lib + "/../build/spec";
   path = dir + "/spec_" + h.hex().substr(0, 24) + ".co";
-  if (access(path.c_str(), R_OK) == 0) return PSG_OK;  // compiled before (by either route)
+  if (access(path.c_str(), R_OK) == 0) return PSG_OK;  // compiled before
   for (size_t i = 1; i <= dir.size(); ++i)  // mkdir -p
     if (i == dir.size() || dir[i] == '/') {
       const std::string d = dir.substr(0, i);
@@ -1291,6 +1367,7 @@ int psg_spec_native_source(const char* text, int32_t alg, int32_t fused, int32_t
     return PSG_EINVAL;
   }
   try {
+    load_options();
     ParsedSpec P = parse_spec(text);
     const Compiled prog = compile_program(P, alg);
     const std::string s = module_source(P, prog, alg, fused != 0, n);
@@ -1309,6 +1386,40 @@ int psg_spec_native_source(const char* text, int32_t alg, int32_t fused, int32_t
   }
 }
 
+int psg_spec_rewrite_text(const char* text, int32_t alg, char* out, size_t* out_len, char* err, size_t err_len) {
+  using namespace psgspec;
+  if (!text || !out_len) {
+    put(err, err_len, "null argument");
+    return PSG_EINVAL;
+  }
+  try {
+    load_options();
+    ParsedSpec P = parse_spec(text);
+    (void)compile_program(P, alg);  // the same checks as the other entry points
+    Tree& T = P.T;
+    std::map<int, int> memo;  // one memo for every root, as codegen_hip shares it
+    std::string s = "(Spec (phase 1)\n  (invariants";
+    for (int inv : P.invs) s += " " + text_of(T, rewrite_vint(T, inv, memo));
+    s += ")\n  (properties";
+    for (auto& p : P.props) s += " (prop \"" + p.first + "\" " + text_of(T, rewrite_vint(T, p.second, memo)) + ")";
+    s += ")";
+    if (P.sp >= 0) s += "\n  (safetyPredicate " + text_of(T, rewrite_vint(T, P.sp, memo)) + ")";
+    s += ")";
+    const size_t cap = *out_len;
+    *out_len = s.size() + 1;
+    if (!out || cap < s.size() + 1) {
+      put(err, err_len, "output buffer too small: " + std::to_string(s.size() + 1) + " bytes needed");
+      return PSG_ERANGE;
+    }
+    std::memcpy(out, s.c_str(), s.size() + 1);
+    put(err, err_len, "");
+    return PSG_OK;
+  } catch (const std::exception& e) {
+    put(err, err_len, e.what());
+    return PSG_EINVAL;
+  }
+}
+
 int psg_spec_compile_native(const char* text, int32_t alg, int32_t fused, int32_t n, const char* cache_dir,
                             psg_spec_program* out, char* names, size_t names_len, char* err, size_t err_len) {
   using namespace psgspec;
@@ -1319,6 +1430,7 @@ int psg_spec_compile_native(const char* text, int32_t alg, int32_t fused, int32_
   std::memset(out, 0, sizeof(*out));
   std::string path, msg;
   try {
+    load_options();
     ParsedSpec P = parse_spec(text);
     const Compiled prog = compile_program(P, alg);
     const std::string s = module_source(P, prog, alg, fused != 0, n);

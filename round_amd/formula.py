@@ -688,864 +688,41 @@ REFERENCE_SPECS = {
 
 
 # --------------------------------------------------------------------------- native lowering (HIP)
-_CSRC = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "csrc")
-_INCLUDE = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(_CSRC)), "include")
-CACHE_DIR = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(_CSRC)),
-                                        "build", "spec")
+# The lowering of a Spec to gfx950 code lives in the library, psg_spec_gen.cpp
+# (psg_spec_compile_native): ONE generator for this DSL and for the C ABI / JVM route
+# (GpuSpec.scala). compile_native writes the Spec as Formula text (to_text below) and has the
+# library lower and compile it in-process (hiprtc), cached under build/spec by a hash of the
+# source, the kernel headers and the compiler identity. The rewrites it applies are exact for
+# every input (psg_spec_rewrite_text exposes them: tests/test_formula.py checks them against
+# the Spec as written under the CPU interpreter); DESIGN.md §5 lists them.
 
+# algorithms whose round kernel a fused module instantiates with the Spec as its check hook
+FUSED_KERNELS = frozenset({abi.PSG_ALG_OTR, abi.PSG_ALG_OTR2, abi.PSG_ALG_LAST_VOTING, abi.PSG_ALG_FLOODMIN,
+                           abi.PSG_ALG_KSET, abi.PSG_ALG_BENOR, abi.PSG_ALG_SLV, abi.PSG_ALG_KSET_ES})
 
-def _c_int(v):
-    return "(-2147483647 - 1)" if v == -(1 << 31) else f"((int32_t){v})"
-
-
-class _Gen:
-    """Formula tree -> C++ expression over psg_spec_native.hpp (template parameter W)."""
-
-    BIN = {"AND": "(int32_t)((({x}) != 0) & (({y}) != 0))", "OR": "(int32_t)((({x}) != 0) | (({y}) != 0))",
-           "IMPL": "(int32_t)((({x}) == 0) | (({y}) != 0))", "EQ": "(int32_t)(({x}) == ({y}))",
-           "NE": "(int32_t)(({x}) != ({y}))", "LT": "(int32_t)(({x}) < ({y}))", "LE": "(int32_t)(({x}) <= ({y}))",
-           "GT": "(int32_t)(({x}) > ({y}))", "GE": "(int32_t)(({x}) >= ({y}))", "ADD": "spec::iadd({x}, {y})",
-           "SUB": "spec::isub({x}, {y})", "MUL": "spec::imul({x}, {y})", "DIV": "spec::idiv({x}, {y})",
-           "MOD": "spec::imod({x}, {y})"}
-
-    def __init__(self, fields_available=None):
-        self.names = {}       # var uid -> (c name, per-lane?, lane-bound pid?)
-        self.k = itertools.count()
-        self.fields = set()
-        self.tags = set()
-        self.fields_available = fields_available
-        self.max_vi = 0
-        self.tuples = {}      # var uid -> {(field, tag): C++ name} (serial quantifier over distinct states)
-        self.init_sets = []   # fields f with an LDS membership set of init(f) (at most 2)
-        self.cse = {}         # structural key of a closed subformula -> C++ name of its hoisted value
-        self.skeys = {}       # _skey memo
-        self.tup_sets = {}    # field tuple of a distinct-state quantifier -> C++ name of its per-check-point TupU
-        self.tup_used = set()  # field tuples used by the function being generated
-        self.memo_slots = {}   # (init set, field) -> memo slot of member_init_own
-        self.uni = False       # lowering for symmetric check points (spec::uniform, psg_spec_native.hpp)
-        self.pvars = set()     # uids of variables bound to a process (a pid in [0, n))
-        self.uft = []          # (field, tag) current / old fields read by the symmetric lowering
-        self.umemo = {}        # (init set, C++ expression) -> memo slot of member_init_u
-
-    def gen(self, e, in_lane, vi_depth):
-        """(C++ expression, depends on the lane)."""
-        k = _skey(e, self.skeys)
-        if k in self.cse:
-            return self.cse[k], False  # a closed subformula computed once per check point
-        if isinstance(e, Lit):
-            return _c_int(e.v), False
-        if isinstance(e, NVal):
-            return "x.n", False
-        if isinstance(e, RVal):
-            return "x.r", False
-        if isinstance(e, CoordVal):
-            return "((x.r / 4) % x.n)", False
-        if isinstance(e, Var):
-            if e.uid not in self.names:
-                raise FormulaError("variable used outside its quantifier")
-            name, lane, _ = self.names[e.uid]
-            return name, lane
-        if isinstance(e, Field):
-            if self.fields_available is not None and e.f not in self.fields_available:
-                raise FormulaError(f"field {e.f} is not part of this algorithm's state")
-            self.fields.add(e.f)
-            self.tags.add(e.tag)
-            if self.uni and e.tag != TAG_INIT:
-                # symmetric check point: every process holds process 0's value
-                if (e.f, e.tag) not in self.uft:
-                    self.uft.append((e.f, e.tag))
-                if isinstance(e.proc, CoordVal) or (isinstance(e.proc, Var) and e.proc.uid in self.pvars):
-                    return f"x.uf({e.tag}, {e.f})", False
-                p, lane = self.gen(e.proc, in_lane, vi_depth)
-                return f"spec::fld_uni<W>(x, {e.tag}, {e.f}, {p})", lane
-            if isinstance(e.proc, Var) and self.names.get(e.proc.uid, (None, False, False))[2]:
-                return f"x.own({e.tag}, {e.f})", True  # the lane's own process
-            if isinstance(e.proc, Var) and e.proc.uid in self.tuples:
-                return self.tuples[e.proc.uid][(e.f, e.tag)], False  # a distinct-state tuple value
-            p, lane = self.gen(e.proc, in_lane, vi_depth)
-            fn = "fld_g" if lane else "fld_u"
-            return f"spec::{fn}<W>(x, {e.tag}, {e.f}, {p})", lane
-        if isinstance(e, Un):
-            a, lane = self.gen(e.x, in_lane, vi_depth)
-            if e.op == "NOT":
-                return f"(int32_t)(({a}) == 0)", lane
-            if e.op == "NEG":
-                return f"spec::isub(0, {a})", lane
-            return f"(int32_t)(({a}) != (-2147483647 - 1))", lane
-        if isinstance(e, Bin):
-            a, la = self.gen(e.x, in_lane, vi_depth)
-            b, lb = self.gen(e.y, in_lane, vi_depth)
-            if e.op in ("AND", "OR", "IMPL") and _expensive(e.y):
-                # skip a quantified right side when no lane needs it (group-uniform test)
-                if not la:
-                    t = {"AND": "({a}) != 0 ? (int32_t)(({b}) != 0) : 0",
-                         "OR": "({a}) != 0 ? 1 : (int32_t)(({b}) != 0)",
-                         "IMPL": "({a}) == 0 ? 1 : (int32_t)(({b}) != 0)"}[e.op]
-                    return "(" + t.format(a=a, b=b) + ")", lb
-                fn = {"AND": "and_sc", "OR": "or_sc", "IMPL": "impl_sc"}[e.op]
-                return f"spec::{fn}<W>(x, {a}, [&]() -> int32_t {{ return {b}; }})", True
-            return self.BIN[e.op].format(x=a, y=b), la or lb
-        if isinstance(e, Contains):
-            val, lane = self.gen(e.e, in_lane, vi_depth)
-            v = f"b{next(self.k)}"
-            own = isinstance(e.e, Var) and self.names.get(e.e.uid, (None, False, False))[2]
-            if isinstance(e.e, CoordVal) or (isinstance(e.e, Var) and e.e.uid in self.pvars):
-                self.pvars.add(e.comp.var.uid)  # a process's pid
-            # A.contains(i) for the lane's own process i: the comprehension's variable is that
-            # process too (its fields are the lane's registers, not a gather)
-            self.names[e.comp.var.uid] = (val, True, True) if own else (v, lane, False)
-            body, lb = self.gen(e.comp.body, in_lane, vi_depth)
-            return f"([&](int32_t {v}) -> int32_t {{ return {body}; }})({val})", lane or lb
-        if isinstance(e, Quant):
-            return self.quant(e, in_lane, vi_depth)
-        raise FormulaError(f"unsupported node {type(e).__name__}")
-
-    def quant(self, q, in_lane, vi_depth):
-        v = f"v{next(self.k)}"
-        if q.kind in ("forall", "exists", "count"):
-            self.pvars.add(q.var.uid)
-            # a variable may be bound by several quantifiers (_split_forall): drop its last binding
-            self.tuples.pop(q.var.uid, None)
-            self.names.pop(q.var.uid, None)
-            if self.uni:
-                got = self._quant_uni(q, v, in_lane, vi_depth)
-                if got is not None:
-                    return got
-            if not in_lane:
-                self.names[q.var.uid] = (v, True, True)
-                body, _ = self.gen(q.body, True, vi_depth)
-                fn = {"forall": "forall_lane", "exists": "exists_lane", "count": "count_lane"}[q.kind]
-                return f"spec::{fn}<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", False
-            mem = _init_member(q)
-            if mem is not None and (mem[0] in self.init_sets or len(self.init_sets) < 2):
-                f, t = mem
-                if f not in self.init_sets:
-                    self.init_sets.append(f)
-                self.fields.add(f)
-                self.tags.add(TAG_INIT)
-                K = self.init_sets.index(f)
-                if (isinstance(t, Field) and t.tag == TAG_CUR and isinstance(t.proc, Var)
-                        and self.names.get(t.proc.uid, (None, False, False))[2]):
-                    # the lane's own current field: memoized probe (member_init_own)
-                    key = (K, t.f)
-                    if key not in self.memo_slots and len(self.memo_slots) < 4:
-                        self.memo_slots[key] = len(self.memo_slots)
-                    if key in self.memo_slots:
-                        self.fields.add(t.f)
-                        self.tags.add(TAG_CUR)
-                        return f"spec::member_init_own<W, {K}, {t.f}, {self.memo_slots[key]}>(x)", True
-                tc, tl = self.gen(t, in_lane, vi_depth)
-                return f"spec::member_init<W, {K}>(x, {tc})", tl
-            flds = _tuple_fields(q)
-            if flds is not None:
-                # the body reads j only through fields: visit each distinct field tuple once
-                # (count: weighted by how many processes hold it)
-                guard = _tuple_guard(q) if flds else []
-                gcode = None
-                if guard:
-                    # A(j) of forall(j => A(j) ==> B) / exists, count(j => A(j) && B): only the
-                    # processes where it holds are visited; evaluated per lane (j = the lane's own)
-                    self.names[q.var.uid] = (v, True, True)
-                    gcode = " & ".join(f"(int32_t)(({self.gen(c, True, vi_depth)[0]}) != 0)" for c in guard)
-                    del self.names[q.var.uid]
-                names = {ft: f"{v}_{k}" for k, ft in enumerate(flds)}
-                self.tuples[q.var.uid] = names
-                for f, tag in flds:
-                    if self.fields_available is not None and f not in self.fields_available:
-                        raise FormulaError(f"field {f} is not part of this algorithm's state")
-                    self.fields.add(f)
-                    self.tags.add(tag)
-                body, lane = self.gen(q.body, in_lane, vi_depth)
-                mode = {"forall": 0, "exists": 1, "count": 2}[q.kind]
-                params = ", ".join(f"int32_t {names[ft]}" for ft in flds)
-                fl = ", ".join(f"spec::Fld<{f}, {tag}>{{}}" for f, tag in flds)
-                if not flds:
-                    return (f"spec::quant_tup<W, {mode}>(x, [&]({params}) -> int32_t {{ return {body}; }})"), lane
-                # per check point: are those fields the same for every (guarded) process (one tuple)?
-                key = tuple(flds) if gcode is None else (tuple(flds), gcode)
-                if key not in self.tup_sets:
-                    self.tup_sets[key] = f"tu{len(self.tup_sets)}"
-                self.tup_used.add(key)
-                fn = "quant_tup_c" if gcode is None else "quant_tup_gc"
-                return (f"spec::{fn}<W, {mode}>(x, {self.tup_sets[key]}, [&]({params}) -> int32_t "
-                        f"{{ return {body}; }}, {fl})"), lane
-            self.names[q.var.uid] = (v, False, False)
-            body, lane = self.gen(q.body, in_lane, vi_depth)
-            fn = {"forall": "forall_ser", "exists": "exists_ser", "count": "count_ser"}[q.kind]
-            return f"spec::{fn}<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", lane
-        self.names[q.var.uid] = (v, False, False)
-        if q.kind == "vbool":
-            body, lane = self.gen(q.body, in_lane, vi_depth)
-            return f"spec::exists_bool<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", lane
-        pins = None if in_lane else _pins(q.body, q.var.uid)
-        if pins is not None:
-            # equality pins: a conjunct P.forall(i => ... && (cond(i) ==> term(i) == v) && ...)
-            # leaves v = term(i) as the only candidate once some process has cond(i); with
-            # none active, the finitization below decides it
-            fq, plist = pins
-            pl = f"p{next(self.k)}"
-            self.names[fq.var.uid] = (pl, True, True)
-            self.pvars.add(fq.var.uid)
-            conds, vals, plane = [], [], False
-            for cond, term in plist:
-                if cond is None:
-                    conds.append("1")
-                else:
-                    cc, cl = self.gen(cond, True, vi_depth)
-                    conds.append(f"(int32_t)(({cc}) != 0)")
-                    plane = plane or cl
-                tc, tl = self.gen(term, True, vi_depth)
-                vals.append(tc)
-                plane = plane or tl
-            act = " | ".join(conds)
-            val = vals[-1]
-            for cc, tc in reversed(list(zip(conds[:-1], vals[:-1]))):
-                val = f"(({cc}) != 0 ? ({tc}) : ({val}))"
-            general, lane_g = self._vint_unpinned(q, v, in_lane, vi_depth)
-            self.names[q.var.uid] = (v, False, False)
-            body, lane_b = self.gen(q.body, in_lane, vi_depth + 1)
-            self.max_vi = max(self.max_vi, vi_depth + 1)
-            if self.uni and not plane:
-                # symmetric check point: every process has the same pin flag and value
-                return (f"spec::pin_uni({act}, {val}, [&](int32_t {v}) -> int32_t {{ return {body}; }}, "
-                        f"[&]() -> int32_t {{ return {general}; }})"), lane_b or lane_g
-            return (f"spec::exists_int_pin<W>(x, [&](int32_t {pl}) -> int32_t {{ return {act}; }}, "
-                    f"[&](int32_t {pl}) -> int32_t {{ return {val}; }}, scratch + {vi_depth} * 64 * W, "
-                    f"[&](int32_t {v}) -> int32_t {{ return {body}; }}, [&]() -> int32_t {{ return {general}; }})"), True
-        return self._vint_unpinned(q, v, in_lane, vi_depth)
-
-    def _quant_uni(self, q, v, in_lane, vi_depth):
-        """A process quantifier on a symmetric check point, or None for the general rules:
-        a body reading its variable only through current / old fields has one value for every
-        process (forall / exists: that value, count: n or 0); P.exists(j => init(j.f) == t)
-        with a group-uniform t is a scalar-memoized set probe."""
-        if _symmetric(q):
-            self.names[q.var.uid] = ("0", False, False)  # never read but through its fields
-            body, lane = self.gen(q.body, in_lane, vi_depth)
-            if lane and not in_lane:
-                # a group-uniform value in a lane register: reduced over the valid lanes
-                fn = {"forall": "forall_lane", "exists": "exists_lane", "count": "count_lane"}[q.kind]
-                return f"spec::{fn}<W>(x, [&](int32_t {v}) -> int32_t {{ return {body}; }})", False
-            if q.kind == "count":
-                return f"(({body}) != 0 ? x.n : 0)", lane
-            return f"(int32_t)(({body}) != 0)", lane
-        mem = _init_member(q)
-        if mem is not None and (mem[0] in self.init_sets or len(self.init_sets) < 2):
-            f, t = mem
-            tc, tl = self.gen(t, in_lane, vi_depth)
-            if tl:
-                return None
-            if f not in self.init_sets:
-                self.init_sets.append(f)
-            self.fields.add(f)
-            self.tags.add(TAG_INIT)
-            K = self.init_sets.index(f)
-            key = (K, tc)
-            if key not in self.umemo and len(self.umemo) < 4:
-                self.umemo[key] = len(self.umemo)
-            if key in self.umemo:
-                return f"spec::member_init_u<W, {K}, {self.umemo[key]}>(x, {tc})", False
-            return f"spec::member_init<W, {K}>(x, {tc})", False
-        return None
-
-    def _vint_unpinned(self, q, v, in_lane, vi_depth):
-        """V.exists over Int: count-guarded candidates, else the general finitization."""
-        self.names[q.var.uid] = (v, False, False)
-        guard = _count_guard(q)
-        if guard is not None:
-            # a conjunct P.filter(i => i.f == v).size >= L restricts the witnesses to values
-            # of f held by >= L processes (runtime L >= 1; else the general finitization)
-            (f, tag), thr, op = guard
-            self.fields.add(f)
-            self.tags.add(tag)
-            tc, tl = self.gen(thr, in_lane, vi_depth)
-            if tl:
-                guard = None
-        if guard is not None:
-            L = f"(({tc}) + 1)" if op == "GT" else f"({tc})"
-            general, lane_g = self._vint_general(q, v, in_lane, vi_depth)
-            self.names[q.var.uid] = (v, False, False)
-            body, lane = self.gen(q.body, in_lane, vi_depth + 1)
-            self.max_vi = max(self.max_vi, vi_depth + 1)
-            if self.uni and tag != TAG_INIT:
-                # symmetric check point: process 0's value is the only one, held by n processes
-                if (f, tag) not in self.uft:
-                    self.uft.append((f, tag))
-                return (f"([&]() -> int32_t {{ const int32_t L_ = {L}; if (L_ >= 1) return "
-                        f"spec::guard_uni<W>(x, x.uf({tag}, {f}), L_, "
-                        f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); return {general}; }})()"), lane or lane_g
-            return (f"([&]() -> int32_t {{ const int32_t L_ = {L}; if (L_ >= 1) return "
-                    f"spec::exists_int_guard<W, {f | (tag << 8)}>(x, x.own({tag}, {f}), x.stage({tag}, {f}), L_, "
-                    f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); return {general}; }})()"), True
-        return self._vint_general(q, v, in_lane, vi_depth)
-
-    def _vint_general(self, q, v, in_lane, vi_depth):
-        """V.exists over Int by finitization over the compared terms (equality-only: no +-1)."""
-        self.names[q.var.uid] = (v, False, False)
-        exprs, fsets = _Compiler.witnesses(_Compiler(), q)
-        eq_only = _eq_only(q)
-        evs = []
-        for t in exprs:
-            c, _ = self.gen(t, in_lane, vi_depth)
-            evs.append(c)
-        for f, tag in fsets:
-            self.fields.add(f)
-            self.tags.add(tag)
-        self.max_vi = max(self.max_vi, vi_depth + 1)
-        body, lane = self.gen(q.body, in_lane, vi_depth + 1)
-        # its value is group-uniform outside a lane quantifier (the candidates are); the general
-        # lowering keeps the conservative lane flag
-        vlane = (in_lane or lane) if self.uni else True
-        ne, nf = len(evs), len(fsets)
-        ev = ", ".join(evs) if evs else "0"
-        fs = ", ".join(str(f | (t << 8)) for f, t in fsets) if fsets else "0"
-        head = (f"([&]() -> int32_t {{ const int32_t ev_[{max(ne, 1)}] = {{{ev}}}; "
-                f"const int32_t fs_[{max(nf, 1)}] = {{{fs}}}; ")
-        lam = f"[&](int32_t {v}) -> int32_t {{ return {body}; }}); }})()"
-        if eq_only:
-            return (head + f"return spec::exists_int_eq<W, {ne}, {nf}>(x, ev_, fs_, scratch + {vi_depth} * 64 * W, "
-                    + lam), vlane
-        # order comparisons: one candidate per breakpoint (exists_int_bp) instead of v-1, v, v+1
-        sh = _breakpoint_shifts(q, exprs, fsets)
-        return (head + f"const uint32_t sh_[{max(ne + nf, 1)}] = {{{', '.join(f'{m}u' for m in sh) or '0u'}}}; "
-                f"return spec::exists_int_bp<W, {ne}, {nf}>(x, ev_, fs_, sh_, scratch + {vi_depth} * 64 * W, "
-                + lam), vlane
-
-
-def _expensive(e) -> bool:
-    """Does e hold a quantifier or a set membership (worth a short circuit)?"""
-    return any(isinstance(x, (Quant, Contains)) for x in _walk(e))
-
-
-def _init_member(q):
-    """P.exists(j => init(j.f) == t) with t free of j: (f, t), else None."""
-    if q.kind != "exists" or not (isinstance(q.body, Bin) and q.body.op == "EQ"):
-        return None
-    uid = q.var.uid
-    for a, b in ((q.body.x, q.body.y), (q.body.y, q.body.x)):
-        if (isinstance(a, Field) and a.tag == TAG_INIT and isinstance(a.proc, Var) and a.proc.uid == uid
-                and uid not in {x.uid for x in _walk(b) if isinstance(x, Var)}):
-            return a.f, b
-    return None
-
-
-def _skey(e, memo):
-    """Structural key of e, bound variables numbered by binding depth from e: two closed
-    subformulas with equal keys are the same formula (common-subformula hoisting finds the
-    repeats of Formula text, where every occurrence is its own tree, as well as those of one
-    Python object)."""
-    got = memo.get(id(e))
-    if got is not None and got[0] is e:  # the key object is kept alive with its entry
-        return got[1]
-
-    def rec(x, env):
-        if isinstance(x, Var):
-            return ("V", env[x.uid]) if x.uid in env else ("free", x.uid)
-        if isinstance(x, Lit):
-            return ("L", x.v)
-        if isinstance(x, NVal):
-            return ("N",)
-        if isinstance(x, RVal):
-            return ("R",)
-        if isinstance(x, CoordVal):
-            return ("K",)
-        if isinstance(x, Field):
-            return ("F", x.f, x.tag, rec(x.proc, env))
-        if isinstance(x, Un):
-            return ("U", x.op, rec(x.x, env))
-        if isinstance(x, Bin):
-            return ("B", x.op, rec(x.x, env), rec(x.y, env))
-        if isinstance(x, Quant):
-            return ("Q", x.kind, rec(x.body, {**env, x.var.uid: len(env)}))
-        if isinstance(x, Contains):
-            return ("C", rec(x.e, env), rec(x.comp.body, {**env, x.comp.var.uid: len(env)}))
-        raise FormulaError(f"unsupported node {type(x).__name__}")
-
-    k = rec(e, {})
-    memo[id(e)] = (e, k)
-    return k
-
-
-def _symmetric(q):
-    """Does the body of process quantifier q read its variable only through current / old
-    fields (no init field, no use as a pid)?"""
-    uid = q.var.uid
-    nvar = nfield = 0
-    for x in _walk(q.body):
-        if isinstance(x, Var) and x.uid == uid:
-            nvar += 1
-        elif isinstance(x, Field) and isinstance(x.proc, Var) and x.proc.uid == uid:
-            if x.tag == TAG_INIT:
-                return False
-            nfield += 1
-    return nvar == nfield
-
-
-def _tuple_fields(q):
-    """Fields (field, tag) through which the body of a process quantifier reads its
-    variable, or None if the variable is used otherwise (compared as a pid, bound by
-    a set membership, ...)."""
-    uid = q.var.uid
-    out = []
-    field_procs = set()
-    for x in _walk(q.body):
-        if isinstance(x, Field) and isinstance(x.proc, Var) and x.proc.uid == uid:
-            field_procs.add(id(x.proc))
-            if (x.f, x.tag) not in out:
-                out.append((x.f, x.tag))
-    for x in _walk(q.body):
-        if isinstance(x, Var) and x.uid == uid and id(x) not in field_procs:
-            return None
-    return out if len(out) <= 4 else None
-
-
-def _tuple_guard(q):
-    """Conjuncts A of forall(j => A && .. ==> B) / exists, count(j => A && .. && B) that read
-    only j's fields (no quantifier, set or other variable): the processes where one fails
-    contribute nothing, so the distinct-state walk visits only those where all hold."""
-    uid = q.var.uid
-    if q.kind == "forall":
-        if not (isinstance(q.body, Bin) and q.body.op == "IMPL"):
-            return []
-        cs = _conjuncts(q.body.x)
-    else:
-        cs = _conjuncts(q.body)
-    return [c for c in cs if _free_vars(c) == {uid} and not _expensive(c)]
-
-
-def _conjuncts(e):
-    if isinstance(e, Bin) and e.op == "AND":
-        return _conjuncts(e.x) + _conjuncts(e.y)
-    return [e]
-
-
-# breakpoint offsets (bit d+1: b = e + d) of an atom `t OP e` with t the V.exists variable
-_BP_SHIFT = {"LE": 2, "GT": 2, "LT": 1, "GE": 1, "EQ": 3, "NE": 3}
-_FLIP = {"LE": "GE", "GE": "LE", "LT": "GT", "GT": "LT", "EQ": "EQ", "NE": "NE"}
-
-
-def _breakpoint_shifts(q, exprs, fsets):
-    """Per candidate source of _Compiler.witnesses (exprs, then field sets): the union of
-    the breakpoint offsets of the atoms comparing the variable with it (exists_int_bp)."""
-    uid = q.var.uid
-    es = [0] * len(exprs)
-    fm = {k: 0 for k in fsets}
-    for x in _walk(q.body):
-        if not (isinstance(x, Bin) and x.op in _BP_SHIFT):
-            continue
-        for a, b, op in ((x.x, x.y, x.op), (x.y, x.x, _FLIP[x.op])):
-            if not (isinstance(a, Var) and a.uid == uid):
-                continue
-            t = _strip(b)
-            if isinstance(t, Field):
-                fm[(t.f, t.tag)] |= _BP_SHIFT[op]
-            else:
-                hit = [i for i, e in enumerate(exprs) if e is t]
-                if not hit:
-                    return [7] * (len(exprs) + len(fsets))  # unmatched source: every offset (exact)
-                for i in hit:
-                    es[i] |= _BP_SHIFT[op]
-    out = es + [fm[k] for k in fsets]
-    return [m if m else 7 for m in out]
-
-
-def _eq_only(q) -> bool:
-    """Is the V.exists variable of q compared with == / != only?"""
-    uid = q.var.uid
-    for x in _walk(q.body):
-        if isinstance(x, Bin) and x.op in ("LT", "LE", "GT", "GE"):
-            for a in (x.x, x.y):
-                if isinstance(a, Var) and a.uid == uid:
-                    return False
-    return True
-
-
-def _pins(body, uid, banned=frozenset()):
-    """Equality pins of the V.exists variable `uid` in `body`: the first top-level conjunct
-    P.forall(i => c1 && c2 && ...) having conjuncts `cond ==> term == v` or `term == v`
-    (cond, term free of v): (that forall, [(cond or None, term)]), else None. A conjunct
-    V.exists(t => B) is searched too, for pins free of t: they constrain v for every t, so
-    they pin v across the inner quantifier (LastVoting: decided ==> decision == v)."""
-    for c in _conjuncts(body):
-        if isinstance(c, Quant) and c.kind == "vint":
-            got = _pins(c.body, uid, banned | {c.var.uid})
-            if got is not None:
-                return got
-            continue
-        if not (isinstance(c, Quant) and c.kind == "forall"):
-            continue
-        out = []
-        for d in _conjuncts(c.body):
-            cond, eq = (d.x, d.y) if isinstance(d, Bin) and d.op == "IMPL" else (None, d)
-            if cond is not None and (uid in _free_vars(cond) or _free_vars(cond) & banned):
-                continue
-            if not (isinstance(eq, Bin) and eq.op == "EQ"):
-                continue
-            for term, other in ((eq.x, eq.y), (eq.y, eq.x)):
-                if (isinstance(other, Var) and other.uid == uid and uid not in _free_vars(term)
-                        and not (_free_vars(term) & banned)):
-                    out.append((cond, term))
-                    break
-        if out:
-            return c, out
-    return None
-
-
-# The swap below is exact but measured slower on LastVoting's majority clause (fused LV
-# n=64: 205 -> 346 ms per 1.25e7 instances, scripts/fused_breakdown.py): the original order
-# finds its witness early (the first value candidate with the first passing round), the
-# swapped one tries every round candidate. Off by default; the tests exercise both.
-SWAP_VINT = False
-
-
-# The symmetric-check-point lowering (spec::uniform); off only for A/B measurements (the C ABI's
-# generator, psg_spec_gen.cpp, always emits it).
+# Generator options, on only for A/B measurements (PSG_SPEC_OPTIONS, include/psg.h): the
+# symmetric-check-point lowering (spec::uniform) and the split foralls / hoisted conjuncts.
 SYMMETRIC_LOWERING = True
-SYMMETRIC_MAX_FIELDS = 6  # (field, tag) pairs compared by spec::uniform; more: no symmetric lowering
-
-
-def _rewrite_vint(e, memo=None):
-    """Rewrites of V.exists over Int for the native lowering, exact for every input (the
-    domain is non-empty and both sides are decided exactly):
-      V.exists(v => V.exists(t => B)) -> V.exists(t => V.exists(v => B)) when v has equality
-        pins in B and t has none (the pinned variable innermost, where one candidate decides it);
-      V.exists(v => A && B(v)) -> A && V.exists(v => B(v)) for the conjuncts A free of v,
-        P.forall conjuncts split first (_split_forall: LastVoting's majority clause evaluates
-        its v- and t-free implications once, not per candidate).
-    Shared subformulas stay shared (memo by object)."""
-    memo = {} if memo is None else memo
-    k = id(e)
-    if k in memo and memo[k][0] is e:  # the key object is kept alive with its entry (ids are reused)
-        return memo[k][1]
-    out = e
-    if (SWAP_VINT and isinstance(e, Quant) and e.kind == "vint" and isinstance(e.body, Quant)
-            and e.body.kind == "vint"
-            and _pins(e.body.body, e.var.uid) is not None and _pins(e.body.body, e.body.var.uid) is None):
-        out = _rewrite_vint(Quant("vint", e.body.var, Quant("vint", e.var, e.body.body)), memo)
-    elif isinstance(e, Quant):
-        b = _rewrite_vint(e.body, memo)
-        out = e if b is e.body else Quant(e.kind, e.var, b)
-        if out.kind == "vint":
-            out = _vint_step(out, memo)
-        elif out.kind in ("exists", "forall") and SPLIT_FORALL:
-            out = _proc_step(out)
-    elif isinstance(e, Bin):
-        x, y = _rewrite_vint(e.x, memo), _rewrite_vint(e.y, memo)
-        out = e if (x is e.x and y is e.y) else Bin(e.op, x, y)
-    elif isinstance(e, Un):
-        x = _rewrite_vint(e.x, memo)
-        out = e if x is e.x else Un(e.op, x)
-    elif isinstance(e, Contains):
-        b, x = _rewrite_vint(e.comp.body, memo), _rewrite_vint(e.e, memo)
-        out = e if (b is e.comp.body and x is e.e) else Contains(Comprehension(e.comp.var, b), x)
-    memo[k] = (e, out)
-    return out
-
-
-# V.exists(v => ... && P.forall(i => A(i) && B(i, v)) && ...): the forall splits into
-# P.forall(A) && P.forall(B) so that A, free of v, leaves the quantifier (_vint_step) when A
-# does cross-lane work (reads another process's field: LastVoting's coord.commit); A of the
-# lane's own fields stays in the forall (a separate forall would cost one more ballot than it
-# saves). Off only for A/B measurements (psg_spec_gen.cpp always splits).
 SPLIT_FORALL = True
 
 
-def _cross(d, uid):
-    """d reads a field of a process other than `uid`, or holds a quantifier / set membership."""
-    for x in _walk(d):
-        if isinstance(x, (Quant, Contains)):
-            return True
-        if isinstance(x, Field) and not (isinstance(x.proc, Var) and x.proc.uid == uid):
-            return True
-    return False
+def compile_native(spec: Spec, alg: Optional[int] = None, cache_dir: str = None, fused: bool = False,
+                   n: Optional[int] = None, defines: Sequence[str] = ()) -> Program:
+    """Lower `spec` to native gfx950 code and return a Program whose module_path
+    psg_run_batch_spec launches instead of the bytecode interpreter (the library's generator,
+    psg_spec_compile_native, on the Spec's Formula text).
 
-
-def _split_forall(c, v, cross_only=True):
-    """P.forall(i => A && B) with conjuncts A free of v (and doing cross-lane work, cross_only)
-    and the rest B -> [P.forall(A), P.forall(B)] (forall distributes over &&: exact)."""
-    if SPLIT_FORALL and isinstance(c, Quant) and c.kind == "forall":
-        ds = _conjuncts(c.body)
-        out = [v not in _free_vars(d) and (not cross_only or _cross(d, c.var.uid)) for d in ds]
-        fr = [d for d, o in zip(ds, out) if o]
-        bd = [d for d, o in zip(ds, out) if not o]
-        if fr and bd:
-            return [Quant("forall", c.var, And(*fr)), Quant("forall", c.var, And(*bd))]
-    return [c]
-
-
-def _proc_step(q):
-    """P.exists(j => A && B(j)) -> A && P.exists(j => B(j)), the same for P.forall (n >= 1: exact),
-    for the conjuncts A free of j, a conjunct P.forall(i => A(i) && B(i, j)) split first
-    (LastVoting's / OTR's P.exists(j => P.forall(i => i.decided && i.decision == init(j.x))):
-    the serial walk over i runs only once every process decided)."""
-    v = q.var.uid
-    cs = [d for c in _conjuncts(q.body) for d in _split_forall(c, v, cross_only=False)]
-    free = [c for c in cs if v not in _free_vars(c)]
-    bound = [c for c in cs if v in _free_vars(c)]
-    if free and bound:
-        return And(*free, Quant(q.kind, q.var, And(*bound)))
-    return q
-
-
-def _vint_step(q, memo):
-    v, body = q.var.uid, q.body
-    cs = [d for c in _conjuncts(body) for d in _split_forall(c, v)]
-    free = [c for c in cs if v not in _free_vars(c)]
-    bound = [c for c in cs if v in _free_vars(c)]
-    if free and bound:
-        return And(*free, Quant("vint", q.var, And(*bound)))
-    return q
-
-
-def _count_guard(q):
-    """A top-level conjunct `P.filter(i => i.f == v).size OP thr` (OP in >, >=, ==; thr
-    free of bound variables) of V.exists(v => body): ((f, tag), thr, OP) or None."""
-    uid = q.var.uid
-    for c in _conjuncts(q.body):
-        if not isinstance(c, Bin) or c.op not in ("GT", "GE", "EQ", "LT", "LE"):
-            continue
-        cnt, thr, op = c.x, c.y, c.op
-        if not (isinstance(cnt, Quant) and cnt.kind == "count"):
-            cnt, thr = c.y, c.x
-            op = {"LT": "GT", "LE": "GE", "EQ": "EQ", "GT": "LT", "GE": "LE"}[c.op]
-        if op not in ("GT", "GE", "EQ") or not (isinstance(cnt, Quant) and cnt.kind == "count"):
-            continue
-        if any(isinstance(x, (Var, Quant, Field, Contains)) for x in _walk(thr)):
-            continue  # the threshold must be uniform (n, r, literals)
-        b = cnt.body
-        if not (isinstance(b, Bin) and b.op == "EQ"):
-            continue
-        for fld, other in ((b.x, b.y), (b.y, b.x)):
-            if (isinstance(fld, Field) and isinstance(fld.proc, Var) and fld.proc.uid == cnt.var.uid
-                    and isinstance(other, Var) and other.uid == uid):
-                return (fld.f, fld.tag), thr, op
-    return None
-
-
-def codegen_hip(spec: Spec, alg: Optional[int] = None) -> Tuple[str, Program]:
-    """HIP source of the native checker of `spec` (+ the bytecode Program it replaces)."""
-    prog = compile_spec(spec, alg)
-    gen = _Gen(ALG_FIELDS.get(alg) if alg is not None else None)
-    guard = _rinv_guard(spec)
-    memo = {}
-    invs = [_rewrite_vint(inv if guard is None else (inv & guard), memo) for inv in spec.invariants]
-    props = [(name, _rewrite_vint(f, memo)) for name, f in spec.properties]
-    safety = None if spec.safety_predicate is None else _rewrite_vint(spec.safety_predicate, memo)
-    # common closed subformulas (the same formula in several places, e.g. OTR's keepInit in
-    # Invariant0 and Invariant1; structurally equal, _skey): hoisted, evaluated once per check point
-    roots = list(invs) + [f for name, f in props if name != "Termination"]
-    if safety is not None:
-        roots.append(safety)
-    seen, order = {}, []
-
-    def visit(e):
-        k = _skey(e, gen.skeys)
-        seen[k] = seen.get(k, 0) + 1
-        if seen[k] > 1:
-            return
-        for c in e.children():
-            visit(c)
-        order.append(e)  # post-order: inner subformulas first
-
-    for rt in roots:
-        visit(rt)
-
-    def tup_decls(used, ind):
-        out = []
-        for k in gen.tup_sets:
-            if k not in used:
-                continue
-            flds, gcode = (k, None) if not (len(k) == 2 and isinstance(k[1], str)) else k
-            fl = ", ".join(f"spec::Fld<{f}, {tag}>{{}}" for f, tag in flds)
-            if gcode is None:
-                out.append(f"{ind}const auto {gen.tup_sets[k]} = spec::tup_uniform<W>(x, {fl});")
-            else:
-                out.append(f"{ind}const auto {gen.tup_sets[k]} = spec::tup_uniform_g<W>(x, {gcode}, {fl});")
-        return out
-
-    def block(uni):
-        """The slot lines of fail() and the Termination expression, under the general or the
-        symmetric-check-point lowering. A distinct-state tuple test is declared just before the
-        first line that uses it (short live ranges: the fused kernels are register-bound)."""
-        gen.uni, gen.cse, gen.tup_used = uni, {}, set()
-        ind, pre = ("      ", "ucse") if uni else ("    ", "cse")
-        lines = []
-
-        def add(e, fmt):
-            before = set(gen.tup_used)
-            c, _ = gen.gen(e, False, 0)
-            lines.extend(tup_decls(gen.tup_used - before, ind))
-            lines.append(fmt(c))
-
-        slot = 0
-        for e in order:
-            if seen[_skey(e, gen.skeys)] > 1 and isinstance(e, (Quant, Contains)) and not _free_vars(e):
-                name = f"{pre}{len(gen.cse)}"
-                add(e, lambda c, name=name: f"{ind}const int32_t {name} = {c};")
-                gen.cse[_skey(e, gen.skeys)] = name
-        iv = "uinv" if uni else "inv"
-        if invs:
-            for k, inv in enumerate(invs):
-                add(inv, lambda c, k=k: f"{ind}const int32_t {iv}{k} = {c};")
-            lines.append(f"{ind}if (!(" + " | ".join(f"({iv}{k} != 0)" for k in range(len(invs)))
-                         + f")) fb |= 1u << {slot};")
-            slot += 1
-            for k in range(len(invs)):
-                lines.append(f"{ind}if ({iv}{k} == 0) fb |= 1u << {slot};")
-                slot += 1
-        term = None
-        term_tups = set()
-        for name, f in props:
-            if name == "Termination":
-                # term() is its own function: fail()'s hoisted subformulas (cse*) and tuple
-                # tests are not in scope there, so it is lowered with neither
-                saved, gen.tup_used = gen.tup_used, set()
-                saved_cse, gen.cse = gen.cse, {}
-                term, _ = gen.gen(f, False, 0)
-                term_tups, gen.tup_used = gen.tup_used, saved
-                gen.cse = saved_cse
-                continue
-            add(f, lambda c, slot=slot, name=name: f"{ind}if (({c}) == 0) fb |= 1u << {slot};  // {name}")
-            slot += 1
-        if safety is not None:
-            add(safety, lambda c, slot=slot: f"{ind}if (({c}) == 0) fb |= 1u << {slot};  // SafetyPredicate")
-            slot += 1
-        assert slot == len(prog.slot_entry)
-        return lines, term, tup_decls(term_tups, ind), slot
-
-    lines, term, term_decls, slot = block(False)
-    # symmetric check points (every process holds the same value of each current / old field
-    # the Spec reads): a second, scalar lowering, chosen per check point by spec::uniform
-    ulines, uterm, uterm_decls, _ = block(True)
-    gen.uni = False
-    # worth its test only with few fields to compare: OTR's 5 (x, decided, decision; old decided,
-    # decision) are symmetric at 86 % of check points (fused OTR 13.4 -> 11.6 ms per 2.5e6
-    # instances), LastVoting's 9 almost never (22.9 -> 24.4 ms: the test is pure overhead)
-    if gen.uft and len(gen.uft) <= SYMMETRIC_MAX_FIELDS and SYMMETRIC_LOWERING:
-        cur = sum(1 << f for f, t in gen.uft if t == TAG_CUR)
-        old = sum(1 << f for f, t in gen.uft if t == TAG_OLD)
-        lines = ([f"    if (spec::uniform<W, {cur}u, {old}u>(x)) {{"] + ulines + ["      return fb;", "    }"]
-                 + lines)
-        if term:
-            term_decls = (["    if (x.uni) {"] + uterm_decls + [f"      return ({uterm}) != 0;", "    }"]
-                          + term_decls)
-    if gen.max_vi > 4:
-        raise FormulaError("more than 4 nested V.exists over Int")
-    rel = sum(1 << s for s, fl in enumerate(prog.slot_flags) if fl & SPEC_RELATIONAL)
-    fmask = sum(1 << f for f in gen.fields)
-    tmask = sum(1 << t for t in gen.tags)
-    src = [
-        "// generated by round_amd/formula.py (codegen_hip): native checker of one Spec",
-        '#include "psg_spec_native.hpp"',
-        "namespace psg {",
-        "struct GenSpec {",
-        f"  static constexpr int kSlots = {slot};",
-        f"  static constexpr uint32_t kRelational = {rel}u;",
-        f"  static constexpr bool kHasTerm = {'true' if term else 'false'};",
-        f"  static constexpr uint32_t kFields = {fmask}u;",
-        f"  static constexpr uint32_t kTags = {tmask}u;",
-        f"  static constexpr int kInitSet0 = {gen.init_sets[0] if len(gen.init_sets) > 0 else -1};",
-        f"  static constexpr int kInitSet1 = {gen.init_sets[1] if len(gen.init_sets) > 1 else -1};",
-        "  template <int W>",
-        "  __device__ static uint32_t fail(spec::Ctx<W>& x, int32_t* scratch) {",
-        "    (void)scratch;",
-        "    uint32_t fb = 0;",
-        *lines,
-        "    return fb;",
-        "  }",
-        "  template <int W>",
-        "  __device__ static bool term(spec::Ctx<W>& x, int32_t* scratch) {",
-        "    (void)scratch;",
-        *term_decls,
-        f"    return ({term or '0'}) != 0;",
-        "  }",
-        "};",
-        "}  // namespace psg",
-        "PSG_SPEC_NATIVE_KERNELS(psg::GenSpec)",
-        f'extern "C" __device__ int32_t psg_spec_alg = {int(alg or 0)};  // checked by psg_run_batch_spec',
-        "",
-    ]
-    return "\n".join(src), prog
-
-
-# algorithm -> (round-kernel source, body template, leading template arguments) for fused modules
-FUSED_KERNELS = {
-    abi.PSG_ALG_OTR: ("psg_otr.hip", "otr_body", "{W}, false"),
-    abi.PSG_ALG_OTR2: ("psg_otr.hip", "otr_body", "{W}, true"),
-    abi.PSG_ALG_LAST_VOTING: ("psg_lv.hip", "lv_body", "{W}"),
-    abi.PSG_ALG_FLOODMIN: ("psg_floodmin.hip", "floodmin_body", "{W}"),
-    abi.PSG_ALG_KSET: ("psg_kset.hip", "kset_body", "{W}"),
-    abi.PSG_ALG_BENOR: ("psg_benor.hip", "benor_body", "{W}"),
-    abi.PSG_ALG_SLV: ("psg_slv.hip", "slv_body", "{W}"),
-    abi.PSG_ALG_KSET_ES: ("psg_kset_es.hip", "kset_es_body", "{W}"),
-}
-
-
-FUSED_WPE = {abi.PSG_ALG_LAST_VOTING: 6}
-
-
-def _fused_source(alg: int, waves: Sequence[int]) -> str:
-    """The algorithm's round kernel instantiated with the generated Spec as its hook:
-    extern "C" psg_fused_a<alg>_w<W> (seeded HO sets) / psg_fused_x_a<alg>_w<W> (explicit)."""
-    import os
-    src, body, targs = FUSED_KERNELS[alg]
-    out = [f'#include "{src}"  // its kernel bodies; host launchers are compiled out (PSG_FUSED_MODULE)']
-    # occupancy target of the W = 1 kernels (0: the compiler's); LastVoting's generated check
-    # otherwise takes 92 VGPRs (5 waves/SIMD): 6 measured 155.6 -> 147.5 ms on C3 (7: no gain)
-    wpe = int(os.environ.get("PSG_FUSED_WPE") or FUSED_WPE.get(alg, 0))
-    for W in waves:
-        threads = 256 if W == 1 else 64 * W
-        attr = f"__attribute__((amdgpu_waves_per_eu({wpe}))) " if W == 1 and wpe > 0 else ""
-        for suffix, xho in (("", "false"), ("x_", "true")):
-            out.append(f'extern "C" __global__ void __launch_bounds__({threads}) {attr}'
-                       f'psg_fused_{suffix}a{alg}_w{W}(psg::KArgs a) {{')
-            out.append(f"  psg::{body}<{targs.format(W=W)}, {xho}, psg::spec::SpecHook<psg::GenSpec>>(a);")
-            out.append("}")
-    return "\n".join(out) + "\n"
-
-
-def compile_native(spec: Spec, alg: Optional[int] = None, cache_dir: str = None, hipcc: str = None,
-                   fused: bool = False, n: Optional[int] = None, defines: Sequence[str] = ()) -> Program:
-    """Lower `spec` to native gfx950 code (hipcc --genco, cached by source hash) and
-    return a Program whose module_path psg_run_batch_spec launches instead of the
-    bytecode interpreter.
-
-    fused=True also instantiates the algorithm's round kernel with the Spec as its
-    check hook (spec::SpecHook): psg_run_batch_spec then runs ONE launch that
-    executes the rounds and evaluates the Spec from registers, with no state trace.
-    `n` (optional) limits the instantiations to that group size's wave count. `defines`: extra
-    preprocessor definitions (e.g. "PSG_PHASE_TIMERS=1" for a profiling module; part of the
-    cache key)."""
-    import hashlib
-    import os
-    import subprocess
-    src, prog = codegen_hip(spec, alg)
-    hdr_names = ["psg_spec_native.hpp", "psg_device.hpp"]
-    if fused:
-        if alg not in FUSED_KERNELS:
-            raise FormulaError("fused lowering needs one of the integer-state algorithms")
-        waves = [(n + 63) // 64] if n is not None else [1, 2, 3, 4]
-        src = "#define PSG_FUSED_MODULE 1\n" + src + _fused_source(alg, waves)
-        hdr_names += [FUSED_KERNELS[alg][0], "psg_kernels.hpp", "psg_packed.hpp"]  # everything it includes
-    cache_dir = cache_dir or CACHE_DIR
-    os.makedirs(cache_dir, exist_ok=True)
-    hdrs = "".join(open(os.path.join(_CSRC, h)).read() for h in hdr_names)
-    dflags = [f"-D{d}" for d in defines]
-    key_src = src + hdrs + open(os.path.join(_INCLUDE, "psg.h")).read() + ("".join(dflags) if dflags else "")
-    key = hashlib.sha256(key_src.encode()).hexdigest()[:24]
-    out = os.path.join(cache_dir, f"spec_{key}.co")
-    if not os.path.exists(out):
-        path = os.path.join(cache_dir, f"spec_{key}.hip")
-        with open(path, "w") as f:
-            f.write(src)
-        cmd = [hipcc or os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), "--genco", "--offload-arch=gfx950", "-O3",
-               "-std=c++17", "-I", _CSRC, "-I", _INCLUDE, *dflags, path, "-o", out + ".tmp"]
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise FormulaError("native spec compile failed:\n" + r.stderr[-4000:])
-        os.replace(out + ".tmp", out)
-    prog.module_path = out
-    return prog
+    fused=True also instantiates the algorithm's round kernel with the Spec as its check hook
+    (spec::SpecHook): psg_run_batch_spec then runs ONE launch that executes the rounds and
+    evaluates the Spec from registers, with no state trace. `n` (optional) limits the
+    instantiations to that group size's wave count. `defines`: preprocessor definitions
+    (e.g. "PSG_PHASE_TIMERS=1" for a profiling module; part of the source, so of the cache key)."""
+    from . import lib
+    if fused and alg not in FUSED_KERNELS:
+        raise FormulaError("fused lowering needs one of the integer-state algorithms")
+    opts = ([] if SYMMETRIC_LOWERING else ["nosym"]) + ([] if SPLIT_FORALL else ["nosplit"])
+    opts += ["D" + d for d in defines]
+    return lib.spec_compile_native(to_text(spec), int(alg or 0), fused, int(n or 0), cache_dir, opts)
 
 
 # --------------------------------------------------------------------------- Formula text (JVM interchange)

@@ -25,7 +25,7 @@ EXPORTED_SYMBOLS = [
     "psg_selftest_map_head", "psg_load_inputs_f64", "psg_copy_decisions_f64", "psg_fetch_instances_f64",
     "psg_run_batch_spec", "psg_load_schedule", "psg_clear_schedule", "psg_materialize_schedule",
     "psg_population_fresh", "psg_population_next", "psg_population_read", "psg_spec_from_text", "psg_spec_release",
-    "psg_spec_compile_native", "psg_spec_native_source", "psg_selftest_bitset",
+    "psg_spec_compile_native", "psg_spec_native_source", "psg_selftest_bitset", "psg_spec_rewrite_text",
 ]
 
 
@@ -85,14 +85,16 @@ def load():
                                               C.c_size_t]
         L.psg_spec_native_source.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
                                              C.POINTER(C.c_size_t), C.c_char_p, C.c_size_t]
+        L.psg_spec_rewrite_text.argtypes = [C.c_char_p, C.c_int32, C.c_char_p, C.POINTER(C.c_size_t), C.c_char_p,
+                                            C.c_size_t]
+        L.psg_selftest_bitset.argtypes = [C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.c_int32,
+                                          C.POINTER(C.c_int32), C.c_int32]
     except AttributeError:
         pass
     L.psg_spec_release.argtypes = [C.POINTER(abi.SpecProgram)]
     L.psg_spec_release.restype = None
     L.psg_selftest_map_head.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_int32,
                                         C.POINTER(C.c_int32)]
-    L.psg_selftest_bitset.argtypes = [C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.c_int32,
-                                      C.POINTER(C.c_int32), C.c_int32]
     _lib = L
     return L
 
@@ -376,18 +378,40 @@ def spec_from_text(text, alg=0):
         L.psg_spec_release(C.byref(cp))
 
 
-def spec_compile_native(text, alg=0, fused=False, n=0, cache_dir=None):
+class _SpecOptions:
+    """PSG_SPEC_OPTIONS (the generator's options, psg.h) for the duration of one call."""
+
+    def __init__(self, options):
+        self.options = ",".join(options)
+
+    def __enter__(self):
+        self.saved = os.environ.get("PSG_SPEC_OPTIONS")
+        if self.options:
+            os.environ["PSG_SPEC_OPTIONS"] = self.options
+        else:
+            os.environ.pop("PSG_SPEC_OPTIONS", None)
+
+    def __exit__(self, *exc):
+        if self.saved is None:
+            os.environ.pop("PSG_SPEC_OPTIONS", None)
+        else:
+            os.environ["PSG_SPEC_OPTIONS"] = self.saved
+
+
+def spec_compile_native(text, alg=0, fused=False, n=0, cache_dir=None, options=()):
     """psg_spec_compile_native (host code, hiprtc, no GPU needed): Formula text -> a
     formula.Program whose module_path is the natively lowered (fused: with the round kernel)
-    code object, compiled in-process by the library."""
+    code object, compiled in-process by the library. options: generator options (psg.h
+    PSG_SPEC_OPTIONS: "nosym", "nosplit", "D<NAME>=<VALUE>")."""
     from . import formula
     L = load()
     cp = abi.SpecProgram()
     err = C.create_string_buffer(8192)
     names = C.create_string_buffer(1 << 16)
-    rc = L.psg_spec_compile_native(text.encode(), int(alg), 1 if fused else 0, int(n),
-                                   cache_dir.encode() if cache_dir else None, C.byref(cp), names, len(names),
-                                   err, len(err))
+    with _SpecOptions(options):
+        rc = L.psg_spec_compile_native(text.encode(), int(alg), 1 if fused else 0, int(n),
+                                       cache_dir.encode() if cache_dir else None, C.byref(cp), names, len(names),
+                                       err, len(err))
     if rc != 0:
         raise formula.FormulaError(err.value.decode() or f"psg_spec_compile_native rc={rc}")
     try:
@@ -404,19 +428,30 @@ def spec_compile_native(text, alg=0, fused=False, n=0, cache_dir=None):
         del path
 
 
-def spec_native_source(text, alg=0, fused=False, n=0):
-    """psg_spec_native_source: the HIP source psg_spec_compile_native compiles (no compile)."""
+def _text_call(fn, name, options, *args):
+    """A psg.h entry point with the (out, *out_len, err, err_len) buffer contract -> str."""
     from . import formula
-    L = load()
     err = C.create_string_buffer(8192)
     size = C.c_size_t(0)
-    rc = L.psg_spec_native_source(text.encode(), int(alg), 1 if fused else 0, int(n), None, C.byref(size), err,
-                                  len(err))
-    if rc not in (0, abi.PSG_ERANGE):
-        raise formula.FormulaError(err.value.decode() or f"psg_spec_native_source rc={rc}")
-    buf = C.create_string_buffer(size.value)
-    rc = L.psg_spec_native_source(text.encode(), int(alg), 1 if fused else 0, int(n), buf, C.byref(size), err,
-                                  len(err))
+    with _SpecOptions(options):
+        rc = fn(*args, None, C.byref(size), err, len(err))
+        if rc not in (0, abi.PSG_ERANGE):
+            raise formula.FormulaError(err.value.decode() or f"{name} rc={rc}")
+        buf = C.create_string_buffer(size.value)
+        rc = fn(*args, buf, C.byref(size), err, len(err))
     if rc != 0:
-        raise formula.FormulaError(err.value.decode() or f"psg_spec_native_source rc={rc}")
+        raise formula.FormulaError(err.value.decode() or f"{name} rc={rc}")
     return buf.value.decode()
+
+
+def spec_native_source(text, alg=0, fused=False, n=0, options=()):
+    """psg_spec_native_source: the HIP source psg_spec_compile_native compiles (no compile)."""
+    L = load()
+    return _text_call(L.psg_spec_native_source, "psg_spec_native_source", options, text.encode(), int(alg),
+                      1 if fused else 0, int(n))
+
+
+def spec_rewrite_text(text, alg=0, options=()):
+    """psg_spec_rewrite_text: the Spec after the native lowering's exact rewrites, as Formula text."""
+    L = load()
+    return _text_call(L.psg_spec_rewrite_text, "psg_spec_rewrite_text", options, text.encode(), int(alg))

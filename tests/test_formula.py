@@ -53,49 +53,6 @@ def test_custom_specs_match_direct_evaluation(cid, alg, n, kw, mk, oracle_mod):
     assert ff == rf and tm == rt
 
 
-def _breakpoint_domain(q, st, env):
-    """The native lowering's candidates for an order-compared V.exists (exists_int_bp):
-    each source's values shifted by its breakpoint offsets, plus Int.MaxValue."""
-    if F._eq_only(q):
-        return st.dom
-    exprs, fsets = F._Compiler().witnesses(q)
-    sh = F._breakpoint_shifts(q, exprs, fsets)
-    vals = [[formula_ref.ev(t, st, env)] for t in exprs]
-    vals += [[st.field(f, tag, p) for p in range(st.n)] for f, tag in fsets]
-    dom = {formula_ref.INT_MAX}
-    for vs, m in zip(vals, sh):
-        for v in vs:
-            dom |= {formula_ref._wrap(v + d) for d in (-1, 0, 1) if (m >> (d + 1)) & 1}
-    return sorted(dom)
-
-
-@pytest.mark.parametrize("cid,alg,n,kw,mk", [c for c in spec_cases.CUSTOM if c[2] <= 16] + [
-    ("lv-ref", psync.LastVoting(), 8, dict(value_range=3, schedule=H(drop_log2=1, good_round=0.0, crash_fmax=3)),
-     F.lv_spec)], ids=[c[0] for c in spec_cases.CUSTOM if c[2] <= 16] + ["lv-ref"])
-def test_breakpoint_finitization_is_exact(cid, alg, n, kw, mk, oracle_mod, monkeypatch):
-    """V.exists over Int decided on the breakpoint candidates (native exists_int_bp) equals
-    the brute-forced domain, check point by check point."""
-    cfg = psync.make_config(alg, n, seed=23, **kw)
-    spec = mk()
-    cnt = 8
-    tr = oracle_mod.trace(cfg, 0, cnt)
-    want = formula_ref.evaluate(spec, tr, cnt, n, cfg.rounds)
-    monkeypatch.setattr(formula_ref, "VINT_DOMAIN", _breakpoint_domain)
-    assert formula_ref.evaluate(spec, tr, cnt, n, cfg.rounds) == want
-
-
-def _rewritten(spec):
-    """The Spec with every formula passed through the native lowering's V.exists rewrites."""
-    memo = {}
-    g = F._rinv_guard(spec)
-    invs = [F._rewrite_vint(inv if g is None else (inv & g), memo) for inv in spec.invariants]
-    props = [(name, F._rewrite_vint(f, memo)) for name, f in spec.properties]
-    sp = None if spec.safety_predicate is None else F._rewrite_vint(spec.safety_predicate, memo)
-    plain = [inv if g is None else (inv & g) for inv in spec.invariants]
-    return (F.Spec(plain, [], spec.properties, spec.safety_predicate, phase_length=spec.phase_length),
-            F.Spec(invs, [], props, sp, phase_length=spec.phase_length))
-
-
 REWRITE_CASES = [(f"ref-{a}", alg, n, kw, F.REFERENCE_SPECS[a]) for a, alg, n, kw in [
     (abi.PSG_ALG_OTR, psync.OTR(), 16, dict(value_range=3, schedule=H(drop_log2=1))),
     (abi.PSG_ALG_OTR2, psync.OTR2(), 10, {}),
@@ -105,36 +62,44 @@ REWRITE_CASES = [(f"ref-{a}", alg, n, kw, F.REFERENCE_SPECS[a]) for a, alg, n, k
     (abi.PSG_ALG_BENOR, psync.BenOr(), 8, {})]] + [c for c in spec_cases.CUSTOM if c[2] <= 16]
 
 
-@pytest.mark.parametrize("swap", [False, True], ids=["hoist", "swap+hoist"])
+def _rewritten(spec, alg_id):
+    """The Spec after the library generator's rewrites (psg_spec_rewrite_text), back in the DSL."""
+    from round_amd import lib
+    return F.from_text(lib.spec_rewrite_text(F.to_text(spec), alg_id))
+
+
 @pytest.mark.parametrize("cid,alg,n,kw,mk", REWRITE_CASES, ids=[c[0] for c in REWRITE_CASES])
-def test_native_rewrites_are_exact(cid, alg, n, kw, mk, oracle_mod, swap, monkeypatch):
-    """The V.exists rewrites of the native lowering (swap to put the pinned variable
-    innermost, hoist conjuncts free of the variable) give the same results as the
-    Spec as written, under the CPU interpreter, check point by check point."""
-    monkeypatch.setattr(F, "SWAP_VINT", swap)
+def test_native_rewrites_are_exact(cid, alg, n, kw, mk, oracle_mod):
+    """The rewrites of the native lowering (psg_spec_gen.cpp: conjuncts free of a bound
+    variable hoisted out of V.exists / P.exists / P.forall, split foralls) give the same
+    results as the Spec as written, under the CPU interpreter, check point by check point."""
     cfg = psync.make_config(alg, n, seed=29, **kw)
-    orig, rw = _rewritten(mk())
+    spec = mk()
     cnt = 300
     tr = oracle_mod.trace(cfg, 0, cnt)
-    f1, t1 = oracle_mod.vm_run(F.compile_spec(orig, alg.alg_id), tr, cnt, n, cfg.rounds)
-    f2, t2 = oracle_mod.vm_run(F.compile_spec(rw, alg.alg_id), tr, cnt, n, cfg.rounds)
+    f1, t1 = oracle_mod.vm_run(F.compile_spec(spec, alg.alg_id), tr, cnt, n, cfg.rounds)
+    f2, t2 = oracle_mod.vm_run(F.compile_spec(_rewritten(spec, alg.alg_id), alg.alg_id), tr, cnt, n, cfg.rounds)
     assert f1 == f2 and t1 == t2
 
 
 def test_rewrites_shapes():
-    """LastVoting's majority clause: the pinned value variable moves innermost and the
-    conjuncts free of it are hoisted out (the lowering then takes one candidate)."""
-    spec = F.lv_spec()
-    F.SWAP_VINT = True
-    try:
-        mb = F._rewrite_vint(spec.invariants[0])
-    finally:
-        F.SWAP_VINT = False
-    vints = [x for x in F._walk(mb) if isinstance(x, F.Quant) and x.kind == "vint"]
-    assert len(vints) == 2
-    outer, inner = vints
-    assert F._pins(inner.body, inner.var.uid) is not None  # v, pinned by x / decision / vote
-    assert F._pins(outer.body, outer.var.uid) is None       # t
+    """The hoisting shapes: V.exists(v => A && B(v)) -> A && V.exists(v => B(v)) for
+    a cross-lane A (LastVoting's `ts == r/4 ==> coord.commit`), and P.exists(j => P.forall(i =>
+    i.decided && i.decision == init(j.x))) -> P.forall(i => i.decided) && P.exists(j => ...)."""
+    P, V, init = F.P, F.V, F.init
+    c = F.coord
+    spec = F.Spec(properties=[
+        ("A", V.exists(lambda v: P.forall(lambda i: (i.ts == F.r // 4).implies(F.Field(F.FIELD_COMMIT, c))
+                                          & i.decided.implies(i.decision == v)))),
+        ("B", P.exists(lambda j: P.forall(lambda i: i.decided & (i.decision == init(j.x)))))])
+    rw = _rewritten(spec, abi.PSG_ALG_LAST_VOTING)
+    a, b = [f for _, f in rw.properties]
+    assert isinstance(a, F.Bin) and a.op == "AND"
+    assert isinstance(a.x, F.Quant) and a.x.kind == "forall"   # the coord.commit implication, out of V.exists
+    assert isinstance(a.y, F.Quant) and a.y.kind == "vint"
+    assert isinstance(b, F.Bin) and b.op == "AND"
+    assert isinstance(b.x, F.Quant) and b.x.kind == "forall"   # P.forall(i => i.decided), hoisted
+    assert isinstance(b.y, F.Quant) and b.y.kind == "exists"
 
 
 def test_custom_specs_find_violations(oracle_mod):
@@ -166,7 +131,7 @@ def test_program_layout():
 
 @pytest.mark.parametrize("name", ["otr", "otr2", "lv", "benor", "custom", "termcse"])
 def test_native_lowering_builds(name):
-    """codegen_hip output compiles for gfx950 (hipcc --genco; no GPU needed)."""
+    """compile_native (the library's generator + hiprtc) builds a gfx950 module (no GPU needed)."""
     specs = {"otr": (F.otr_spec, abi.PSG_ALG_OTR), "otr2": (F.otr2_spec, abi.PSG_ALG_OTR2),
              "lv": (F.lv_spec, abi.PSG_ALG_LAST_VOTING), "benor": (F.benor_spec, abi.PSG_ALG_BENOR),
              "custom": (spec_cases.lv_custom, abi.PSG_ALG_LAST_VOTING),
@@ -185,30 +150,26 @@ def test_fused_lowering_builds(alg):
     prog = F.compile_native(spec, alg, fused=True, n=64)
     import os
     assert os.path.getsize(prog.module_path) > 1000
-    src = F._fused_source(alg, [1]) + F.codegen_hip(spec, alg)[0]  # what the module was built from
+    from round_amd import lib
+    src = lib.spec_native_source(F.to_text(spec), alg, True, 64)  # what the module was built from
     assert f"psg_fused_a{alg}_w1" in src and f"psg_fused_x_a{alg}_w1" in src
     assert f"psg_spec_alg = {alg};" in src and prog.alg == alg
 
 
-def test_symmetric_and_guard_classification():
-    """The shape analyses behind the symmetric-check-point lowering (_symmetric: a process
-    variable read only through current / old fields) and the guarded distinct-state walk
-    (_tuple_guard: the conjuncts that read only the quantified process)."""
-    P, init, old = F.P, F.init, F.old
+def test_lowering_shapes_in_source():
+    """The shape analyses of the generator, read off the source it emits: a nested process
+    quantifier whose body reads its variable only through fields walks the distinct field
+    tuples (quant_tup), guarded by the implication's conjuncts that read only that process
+    (tup_uniform_g), unguarded otherwise; the symmetric-check-point lowering (spec::uniform)
+    goes with the "nosym" option."""
+    from round_amd import lib
+    P = F.P
 
-    def q(mk):
-        e = mk()
-        assert isinstance(e, F.Quant)
-        return e
-    assert F._symmetric(q(lambda: P.forall(lambda i: i.decided.implies(i.decision == old(i.decision)))))
-    assert not F._symmetric(q(lambda: P.forall(lambda i: i.x == init(i.x))))  # reads init
-    A = P.filter(lambda i: i.decided)
-    assert not F._symmetric(q(lambda: P.forall(lambda i: A.contains(i))))  # used as a pid
-    # forall(j => A(j) ==> B): the conjuncts of A reading only j
-    g = F._tuple_guard(q(lambda: P.forall(lambda j: (j.decided & (j.x > 0)).implies(j.decision == 3))))
-    assert len(g) == 2
-    outer = F.Var("proc")
-    g = F._tuple_guard(q(lambda: P.forall(lambda j: (outer.decided & j.decided).implies(j.decision == outer.x))))
-    assert len(g) == 1  # outer.decided reads another process
-    assert F._tuple_guard(q(lambda: P.exists(lambda j: j.decided & (j.decision == outer.x)))) != []
-    assert F._tuple_guard(q(lambda: P.forall(lambda j: j.decided & (j.decision == 1)))) == []  # not an implication
+    def src(f, **kw):
+        return lib.spec_native_source(F.to_text(F.Spec(properties=[("X", f)])), abi.PSG_ALG_OTR, **kw)
+    guarded = src(P.exists(lambda i: P.forall(lambda j: (j.decided & (j.x > 0)).implies(j.decision == i.x))))
+    assert "quant_tup" in guarded and "tup_uniform_g" in guarded
+    plain = src(P.exists(lambda i: P.forall(lambda j: j.decided & (j.decision == i.x))))
+    assert "quant_tup" in plain and "tup_uniform_g" not in plain and "tup_uniform<" in plain
+    assert "spec::uniform<" in plain and "spec::uniform<" not in src(
+        P.exists(lambda i: P.forall(lambda j: j.decided & (j.decision == i.x))), options=["nosym"])

@@ -2,14 +2,13 @@
 
 The JVM plugin hands a psync.Spec to the library as Formula text (integration/scala/
 GpuSpec.scala). psg_spec_from_text compiles it to bytecode; psg_spec_compile_native also
-lowers it to native gfx950 code in-process — the generator of round_amd/formula.py
-(codegen_hip, _fused_source) restated in C++ (round_amd/csrc/psg_spec_gen.cpp), compiled
-with hiprtc, cached under formula.compile_native's key. CPU tests: the C++ source is byte
-for byte the one Python generates from the same text (formula.from_text), for the reference
-Specs, every custom Spec of the GPU suites and FormulaExtractor-shaped texts, native and
-fused; a hiprtc compile yields a gfx950 code object whose program equals psg_spec_from_text's.
-GPU tests: the library-compiled fused module's results equal the built-in checker's and the
-Python-compiled module's, word for word.
+lowers it to native gfx950 code in-process (round_amd/csrc/psg_spec_gen.cpp, compiled with
+hiprtc). It is the only generator: formula.compile_native writes a DSL Spec as Formula text and
+calls it, so the DSL and the JVM routes build the same module. CPU tests: every
+reference and custom Spec of the GPU suites and the FormulaExtractor-shaped texts lower, native
+and fused; the DSL -> text -> DSL round trip lowers to the same source; a hiprtc compile yields a gfx950 code
+object whose program equals psg_spec_from_text's. GPU tests: the library-compiled fused module's
+results equal the built-in checker's, word for word.
 """
 import os
 
@@ -20,14 +19,6 @@ from round_amd import abi, formula as F, lib, psync
 import spec_cases
 import test_spec_text as TT
 
-
-def _python_source(text, alg, fused, n):
-    src, _ = F.codegen_hip(F.from_text(text), alg)
-    if fused:
-        src = "#define PSG_FUSED_MODULE 1\n" + src + F._fused_source(alg, [(n + 63) // 64])
-    return src
-
-
 CASES = [(f"ref-{a}", a, 64, lambda a=a: F.to_text(F.REFERENCE_SPECS[a]())) for a in sorted(F.REFERENCE_SPECS)]
 CASES += [(c[0], c[1].alg_id, c[2], lambda mk=c[4]: F.to_text(mk())) for c in spec_cases.CUSTOM]
 CASES += [("let", abi.PSG_ALG_LAST_VOTING, 8, lambda: TT.LV_MAJORITY_LET),
@@ -36,12 +27,36 @@ CASES += [("let", abi.PSG_ALG_LAST_VOTING, 8, lambda: TT.LV_MAJORITY_LET),
 
 
 @pytest.mark.parametrize("cid,alg,n,text", CASES, ids=[c[0] for c in CASES])
-def test_native_source_equals_python(cid, alg, n, text):
+def test_native_source_generates(cid, alg, n, text):
+    """Every Spec lowers (native and fused), the fused module holds the algorithm's kernels
+    for n's wave count, and the DSL route reaches the same generator with the same text."""
     t = text()
     for fused in (False, True):
         if fused and alg not in F.FUSED_KERNELS:
             continue
-        assert lib.spec_native_source(t, alg, fused, n) == _python_source(t, alg, fused, n), (cid, fused)
+        src = lib.spec_native_source(t, alg, fused, n)
+        assert "struct GenSpec" in src and f"psg_spec_alg = {alg};" in src, (cid, fused)
+        if fused:
+            W = (n + 63) // 64
+            assert f"psg_fused_a{alg}_w{W}(" in src and f"psg_fused_x_a{alg}_w{W}(" in src
+    assert lib.spec_native_source(F.to_text(F.from_text(t)), alg) == lib.spec_native_source(t, alg)
+
+
+def test_generator_options():
+    """PSG_SPEC_OPTIONS (psg.h): nosym drops the symmetric-check-point lowering, nosplit the
+    split foralls, D<NAME>=<VALUE> adds a #define; the default source has neither change."""
+    t = F.to_text(F.otr_spec())
+    base = lib.spec_native_source(t, abi.PSG_ALG_OTR)
+    assert "spec::uniform<" in base and "spec::uniform<" not in lib.spec_native_source(t, abi.PSG_ALG_OTR,
+                                                                                      options=["nosym"])
+    assert lib.spec_native_source(t, abi.PSG_ALG_OTR, options=["DPSG_PHASE_TIMERS=1"]).startswith(
+        "#define PSG_PHASE_TIMERS 1\n")
+    lv = F.to_text(F.lv_spec())
+    assert lib.spec_native_source(lv, abi.PSG_ALG_LAST_VOTING) != lib.spec_native_source(
+        lv, abi.PSG_ALG_LAST_VOTING, options=["nosplit"])
+    with pytest.raises(F.FormulaError, match="unknown option"):
+        lib.spec_native_source(t, abi.PSG_ALG_OTR, options=["bogus"])
+    assert "PSG_SPEC_OPTIONS" not in os.environ
 
 
 def test_native_source_rejects_like_the_bytecode_compiler():
@@ -63,7 +78,7 @@ def test_hiprtc_compile_on_the_host(tmp_path):
     mtime = os.path.getmtime(prog.module_path)
     again = lib.spec_compile_native(text, abi.PSG_ALG_OTR, True, 64, cache_dir=str(tmp_path))
     assert again.module_path == prog.module_path and os.path.getmtime(again.module_path) == mtime
-    # the cache key is formula.compile_native's: the Python route finds this very file
+    # formula.compile_native is this route: the DSL Spec finds this very file
     assert F.compile_native(F.from_text(text), abi.PSG_ALG_OTR, fused=True, n=64,
                             cache_dir=str(tmp_path)).module_path == prog.module_path
 
@@ -78,8 +93,8 @@ def test_hiprtc_compile_on_the_host(tmp_path):
 def test_text_fused_module_equals_builtin_and_python(alg, mk, n, count, kw):
     """The Spec given as text, lowered and compiled by the library (hiprtc; built into the
     default cache by __graft_entry__.build(), scripts/precompile_specs.py), run fused: every
-    counter and per-instance result equals the built-in checker's and the Python-compiled
-    module's (hipcc, from the DSL Spec), word for word."""
+    counter and per-instance result equals the built-in checker's and the DSL route's
+    (formula.compile_native), word for word."""
     text = F.to_text(mk())
     prog_c = lib.spec_compile_native(text, alg.alg_id, True, n)
     prog_py = F.compile_native(mk(), alg.alg_id, fused=True, n=n)
