@@ -84,8 +84,6 @@ static const uint32_t ROUND_INIT = 0xFFFFFFFFu;
 static const uint32_t ROUND_CRASH = 0xFFFFFFFEu;
 static const uint32_t PID_GLOBAL = 0xFFFFu;
 static const uint32_t COIN_TAG = 0x80000000u;
-/* survival stream of a crashing sender: call index 0x4000 + s (ctr3 = q + (0x4000 + s) << 16) */
-static const uint32_t SURV_TAG = 0x40000000u;
 
 /* 64-bit random word j of stream (inst, round, ctr3base): Philox call s = j/2
  * with counter (inst_lo, inst_hi, round, ctr3base + (s << 16)); even j takes
@@ -216,26 +214,19 @@ struct Schedule {
       base = full & ~drop_bits((uint32_t)k, (uint32_t)p, 0);
     }
     if (cfg.sched.crash_fmax >= 0) {
-      /* a process crashed before round k sends nothing; in its crash round each outgoing link
-       * q -> p survives with bit p & 63 of word p >> 6 of q's own survival stream */
+      Bits half;
+      uint32_t d = cfg.sched.drop_log2;
+      for (int w = 0; w < W; ++w)
+        half |= word_to_bits(w, rword(cfg.seed, inst, (uint32_t)k, (uint32_t)p, (uint32_t)W * d + (uint32_t)w));
       for (int q = 0; q < n; ++q) {
         int cr = crash_round[q];
         if (cr < 0) continue;
-        if (cr < k) base.reset(q);
-        else if (cr == k && !surv(k, q, p)) base.reset(q);
+        if (cr < k || (cr == k && !half.test(q))) base.reset(q);
       }
     }
     if (cfg.sched.self_bit) base.set(p);
     if (cfg.sched.ho_min >= 0 && (int)base.count() <= cfg.sched.ho_min) base = full;
     return base;
-  }
-
-  /* link q -> p survives q's crash round k (sender-keyed: the crashing sender draws the bits
-   * of all its receivers, W words, so a round costs Philox calls per crashing sender, not per
-   * receiver) */
-  bool surv(int k, int q, int p) const {
-    uint64_t w = rword(cfg.seed, inst, (uint32_t)k, SURV_TAG | (uint32_t)q, (uint32_t)(p >> 6));
-    return (w >> (p & 63)) & 1;
   }
 
   int32_t init_value(int p) const {

@@ -70,8 +70,7 @@ struct BoXch {
 };
 
 template <int W, class SC>
-PSG_DEV void benor_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashSets<W>& cs,
-                        BoXch<W> (&X)[2],
+PSG_DEV void benor_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashSets<W>& cs, BoXch<W> (&X)[2],
                         int32_t x0, BlockCounters* bc) {
   const int n = a.n;
   const int thr = a.variant == 1 ? n / 4 : n / 2;  // BenOr.scala:68, 71 (variant 1: mutation)
@@ -144,7 +143,7 @@ PSG_DEV void benor_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashSets
       const bool good = sc.good_round(k, g.lane, a.R, goodS);
       Mask<W> CB = mzero<W>(), CN = mzero<W>();
       if (sc.crash_on) cs.sets(g, k, CB, CN);
-      const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, crash_drop<W>(sc, k, CN, g.wv, g.lane, g.lane)), act);
+      const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
       const int size = mpopc(M);
       predw = !halted && size <= n / 2;
       if ((k & 1) == 0) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
@@ -296,15 +295,12 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
           CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
         }
       }
-      Surv<W> rs;  // crash-round survival words of this round's crashing senders (sender-keyed)
-      rs.prep(sc, k, CN, P.lane);
       constexpr bool even = RS == 0;
       const Mask<W> A1 = mand(T1, act), A2 = mand(T2, act);  // R0: x / canDecide; R1: vote true / false
 #pragma unroll
       for (int j = 0; j < W; ++j) {
-        const Mask<W> CNd = rs.drop(sc, k, j, P.lane, P.lane);  // converged: readlanes of the crashing senders
         if (halted[j]) continue;  // a halted process neither receives nor updates
-        const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CNd), act);
+        const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
         const int size = mpopc(M);
         predw[j] = P.val[j] & (size <= n / 2 ? 1u : 0u);
         if constexpr (even) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
@@ -435,7 +431,7 @@ PSG_DEV void benor_body(const KArgs& a) {
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) cs.sets(g, k, CB, CN);
-        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, crash_drop<W>(sc, k, CN, g.wv, g.lane, g.lane)), act);
+        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const int size = mpopc(M);
         pt.mark(1);
         if (!halted) hs = size;

@@ -169,8 +169,6 @@ constexpr uint32_t ROUND_INIT = 0xFFFFFFFFu;
 constexpr uint32_t ROUND_CRASH = 0xFFFFFFFEu;
 constexpr uint32_t PID_GLOBAL = 0xFFFFu;
 constexpr uint32_t COIN_TAG = 0x80000000u;
-// survival stream of a crashing sender q (round = its crash round): ctr3 = q + (0x4000 + s) << 16
-constexpr uint32_t SURV_TAG = 0x40000000u;
 
 // ---------------------------------------------------------------- Philox4x32-10
 struct U4 { uint32_t x, y, z, w; };
@@ -446,21 +444,6 @@ PSG_DEV int mfirst(const Mask<W>& a) {
   for (int i = 0; i < W; ++i)
     if (a.w[i]) return i * 64 + __builtin_ctzll(a.w[i]);
   return -1;
-}
-// First set pid of a non-empty mask, cleared from it (word-wise selects: a dynamic
-// word index would send the mask to scratch memory).
-template <int W>
-PSG_DEV int mtake_first(Mask<W>& a) {
-  int q = 0;
-  bool done = false;
-#pragma unroll
-  for (int i = 0; i < W; ++i) {
-    const bool here = !done && a.w[i] != 0ull;
-    q = here ? i * 64 + (int)__builtin_ctzll(a.w[i]) : q;
-    a.w[i] = here ? a.w[i] & (a.w[i] - 1ull) : a.w[i];
-    done = done || here;
-  }
-  return q;
 }
 // last set pid (-1 if empty)
 template <int W>
@@ -960,15 +943,22 @@ struct Sched {
     return good;
   }
 
-  // Raw drop words of HO(pid) in round k, drawn in one straight-line pass over the
-  // Philox calls of pid's stream (no divergent word cache): word j < W*drop feeds drop
-  // mask j / drop (dm[w] = AND of word w's drop words). good: no words are needed (the
-  // round's common set replaces them).
-  PSG_DEV void draw(uint32_t k, uint32_t pid, bool good, uint64_t (&dm)[W]) const {
-    const uint32_t j1 = good ? 0u : (uint32_t)W * drop;
+  // Raw random words of HO(pid) in round k, drawn in one straight-line pass over
+  // the Philox calls of pid's stream (no divergent word cache): word j < W*drop
+  // feeds drop mask j / drop (dm[w] = AND of word w's drop words), word W*drop + w
+  // is the crash-round survival mask hf[w] of word w. good: the drop words are not
+  // needed (the round's common set replaces them); crash = false: the survival
+  // words are not needed (no process crashes in round k) and hf stays all-ones.
+  PSG_DEV void draw(uint32_t k, uint32_t pid, bool good, bool crash, uint64_t (&dm)[W], uint64_t (&hf)[W]) const {
+    const uint32_t nd = (uint32_t)W * drop;
+    const uint32_t j0 = good ? nd : 0u;
+    const uint32_t j1 = crash ? nd + (uint32_t)W : (good ? 0u : nd);
 #pragma unroll
-    for (int w = 0; w < W; ++w) dm[w] = ~0ull;
-    for (uint32_t sidx = 0; 2 * sidx < j1; ++sidx) {
+    for (int w = 0; w < W; ++w) {
+      dm[w] = ~0ull;
+      hf[w] = ~0ull;
+    }
+    for (uint32_t sidx = j0 >> 1; 2 * sidx < j1; ++sidx) {
       const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), k, pid + (sidx << 16), (uint32_t)seed,
                             (uint32_t)(seed >> 32));
       const uint64_t wlo = (uint64_t)o.x | ((uint64_t)o.y << 32);
@@ -976,45 +966,39 @@ struct Sched {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const uint32_t j = 2 * sidx + (uint32_t)h;
-        if (j >= j1) continue;
-        const uint32_t wi = j / drop;
+        const uint64_t word = h ? whi : wlo;
+        if (j < j0 || j >= j1) continue;
+        if (j < nd) {
+          const uint32_t wi = j / drop;
 #pragma unroll
-        for (int w = 0; w < W; ++w)
-          if (wi == (uint32_t)w) dm[w] &= h ? whi : wlo;
+          for (int w = 0; w < W; ++w)
+            if (wi == (uint32_t)w) dm[w] &= word;
+        } else {
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            if (j - nd == (uint32_t)w) hf[w] = word;
+        }
       }
     }
   }
 
-  // The W survival words of crashing sender q in its crash round k: the link q -> p
-  // survives iff bit p & 63 of word p >> 6 is set (sender-keyed, DESIGN §3: a crash round
-  // costs Philox calls per crashing sender, W / 2 each, instead of per receiver).
-  PSG_DEV void surv_words(uint32_t k, uint32_t q, uint64_t (&v)[W]) const {
-#pragma unroll
-    for (int s = 0; 2 * s < W; ++s) {
-      const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), k, (SURV_TAG | q) + ((uint32_t)s << 16),
-                            (uint32_t)seed, (uint32_t)(seed >> 32));
-      v[2 * s] = (uint64_t)o.x | ((uint64_t)o.y << 32);
-      if (2 * s + 1 < W) v[2 * s + 1] = (uint64_t)o.z | ((uint64_t)o.w << 32);
-    }
-  }
-
-  // HO(pid) from its drop words. CB = processes crashed before round k, CNd = those
-  // crashing in round k whose message does not reach pid (Surv::drop; uniform CB).
-  PSG_DEV Mask<W> assemble(int pid, bool good, const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CNd,
-                           const uint64_t (&dm)[W]) const {
+  // HO(pid) from its raw words. CB = processes crashed before round k, CN =
+  // crashing in round k (uniform).
+  PSG_DEV Mask<W> assemble(int pid, bool good, const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CN,
+                           const uint64_t (&dm)[W], const uint64_t (&hf)[W]) const {
     Mask<W> base;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
       base.w[w] = good ? goodS.w[w] : (drop > 0 ? full.w[w] & ~dm[w] : full.w[w]);
-      if (crash_on) base.w[w] &= ~(CB.w[w] | CNd.w[w]);
+      if (crash_on) base.w[w] &= ~(CB.w[w] | (CN.w[w] & ~hf[w]));
     }
     if (self_bit) mset(base, pid);
     if (ho_min >= 0 && mpopc(base) <= ho_min) base = full;
     return base;
   }
 
-  // HO(p) for this lane's process p in round k (CNd: crash_drop / Surv::drop for p).
-  PSG_DEV Mask<W> ho(int k, int pid, bool good, const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CNd) const {
+  // HO(p) for this lane's process p in round k.
+  PSG_DEV Mask<W> ho(int k, int pid, bool good, const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CN) const {
     if constexpr (XHO) {  // explicit: W contiguous words per process, the wave reads 512*W contiguous bytes
       Mask<W> m = mzero<W>();
       if (pid < nproc) {
@@ -1024,81 +1008,11 @@ struct Sched {
       }
       return m;
     }
-    uint64_t dm[W];
-    draw((uint32_t)k, (uint32_t)pid, good, dm);
-    return assemble(pid, good, goodS, CB, CNd, dm);
+    uint64_t dm[W], hf[W];
+    draw((uint32_t)k, (uint32_t)pid, good, crash_on && many(CN), dm, hf);
+    return assemble(pid, good, goodS, CB, CN, dm, hf);
   }
 };
-
-// Survival bits of one round's crashing senders, sender-keyed (Sched::surv_words): lane t
-// holds the W survival words of the t-th crashing sender of the round (ascending pid, 64
-// at a time: one vector pass of W / 2 Philox calls, however many receivers); a receiver
-// reads its bit of each crashing sender with one readlane per word. Round-local (no state
-// kept across rounds: the kernels are register-bound). Every call must come from converged
-// control flow (the lanes holding the words must be active).
-template <int W>
-struct Surv {
-  Mask<W> cn;     // the round's crashing senders (uniform)
-  int ncr;        // |cn|
-  int chunk;      // which 64 crashing senders v holds (-1: none)
-  uint64_t v[W];  // lane t: words of crashing sender 64 * chunk + t
-
-  template <class SC>
-  PSG_DEV void fill(const SC& sc, int k, int c, int lane) {
-    chunk = c;
-    Mask<W> rem = cn;
-    int myq = -1;
-    const int t0 = 64 * c, t1 = min(ncr, t0 + 64);
-    for (int t = 0; t < t1; ++t) {
-      const int q = mtake_first(rem);
-      myq = (t >= t0 && lane == t - t0) ? q : myq;
-    }
-#pragma unroll
-    for (int w = 0; w < W; ++w) v[w] = ~0ull;
-    if (myq >= 0) sc.surv_words((uint32_t)k, (uint32_t)myq, v);
-  }
-  template <class SC>
-  PSG_DEV void prep(const SC& sc, int k, const Mask<W>& CN, int lane) {
-    cn = CN;
-    ncr = mpopc(CN);
-    chunk = -1;
-    if (ncr > 0) fill(sc, k, 0, lane);
-  }
-  // word wd of the t-th crashing sender's survival words (t < ncr, wd uniform): bit b is the
-  // link to receiver 64 * wd + b
-  template <class SC>
-  PSG_DEV uint64_t word(const SC& sc, int k, int t, int wd, int lane) {
-    if ((t >> 6) != chunk) fill(sc, k, t >> 6, lane);  // more than 64 crash in one round
-    uint64_t x = v[0];
-#pragma unroll
-    for (int w = 1; w < W; ++w) x = w == wd ? v[w] : x;
-    return readlane64(x, t & 63);
-  }
-  // the crashing senders whose message does not reach receiver 64 * wd + bit (wd uniform;
-  // bit = the lane for the lane's own receiver, or a uniform value)
-  template <class SC>
-  PSG_DEV Mask<W> drop(const SC& sc, int k, int wd, int bit, int lane) {
-    Mask<W> d = mzero<W>();
-    Mask<W> rem = cn;
-    for (int t = 0; t < ncr; ++t) {
-      const int q = mtake_first(rem);
-      const uint64_t lost = ~(word(sc, k, t, wd, lane) >> bit) & 1ull;
-#pragma unroll
-      for (int w = 0; w < W; ++w) d.w[w] |= (q >> 6) == w ? lost << (q & 63) : 0ull;
-    }
-    return d;
-  }
-};
-
-// The senders crashing in round k (CN, uniform) whose message does not reach receiver
-// 64 * wd + bit: empty unless some process crashes in round k. Converged control flow.
-template <int W, class SC>
-PSG_DEV Mask<W> crash_drop(const SC& sc, int k, const Mask<W>& CN, int wd, int bit, int lane) {
-  if (!sc.crash_on || !many(CN)) return mzero<W>();
-  Surv<W> s;
-  s.prep(sc, k, CN, lane);
-  return s.drop(sc, k, wd, bit, lane);
-}
 
 // Crash sets of round k: CB = processes crashed before round k, CN = crashing in
 // round k. A process's crash round is fixed per instance, so for W > 1 the

@@ -166,7 +166,7 @@ epsilon_kernel(KArgs a) {
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) cs.sets(g, k, CB, CN);
-        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, crash_drop<W>(sc, k, CN, g.wv, g.lane, g.lane)), act);
+        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const Mask<W> Fl = mand(g.ballot(!(k <= maxR)), act);  // senders announcing their halt
         const Mask<W> U = mor(M, H);                             // V = mailbox ++ halted.values
         const int m = mpopc(U);

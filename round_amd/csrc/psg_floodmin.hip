@@ -22,7 +22,7 @@ struct FmLds {
 // Seeded crash-stop schedules without benign loss, good rounds or ho_min (the C4
 // family): HO(p, k) = all \ (CB_k | (CN_k \ S_p)), where CB_k = crashed before k,
 // CN_k = crashing in k and S_p = the senders whose crash-round message reaches p
-// (their survival words' bits for p, sender-keyed), plus p itself. So FloodMin's update (FloodMin.scala:25-31)
+// (p's survival words), plus p itself. So FloodMin's update (FloodMin.scala:25-31)
 //   x(p) = min(x(p), min{x_q : q in HO(p) & alive})
 // is min(x(p), m_U, min{x_q : q in CN_k & alive & S_p}) with m_U the group minimum
 // over U = alive \ (CB_k | CN_k): one group reduction, plus a per-receiver pass over
@@ -120,7 +120,8 @@ PSG_DEV void floodmin_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashS
       const Mask<W> CNa = mand(CN, act);
       int32_t nx = min(x, mU);
       if (many(CNa)) {  // crash round of some alive sender: its message reaches p iff p's survival bit
-        const Mask<W> lost = crash_drop<W>(sc, k, CNa, g.wv, g.lane, g.lane);
+        uint64_t dm[W], hf[W];
+        sc.draw((uint32_t)k, (uint32_t)g.pid, false, true, dm, hf);
         Mask<W> rem = CNa;
         while (many(rem)) {
           const int q = mfirst(rem);
@@ -128,7 +129,11 @@ PSG_DEV void floodmin_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashS
           int32_t xq;
           if constexpr (W == 1) xq = readlane32(x, q);
           else xq = rfl32(F.xs[k & 1][q]);
-          if (!mtest(lost, q)) nx = min(nx, xq);
+          uint64_t word = hf[0];
+#pragma unroll
+          for (int w = 1; w < W; ++w)
+            if ((q >> 6) == w) word = hf[w];
+          if ((word >> (q & 63)) & 1ull) nx = min(nx, xq);
         }
       }
       if (!halted) {
@@ -153,9 +158,9 @@ PSG_DEV void floodmin_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashS
 // The same computation as floodmin_fast for n > 64, one wave per instance with the W
 // processes l + 64 j in lane l (psg_packed.hpp): the check's ballots are wave ballots
 // (existential ones of the lane's OR over its slots), the minima are wave reductions
-// of the lane's minimum over its slots, and a round needs no barrier at all. A crash round
-// reads each receiver's bit of the crashing senders' survival words (Surv: drawn per crashing
-// sender, sender-keyed) instead of drawing receiver words.
+// of the lane's minimum over its slots, and a round needs no barrier at all. Only the
+// survival words of the crashing senders' 64-pid words are drawn (one Philox call per
+// two words), where the group path draws all W.
 template <int W>
 PSG_DEV void floodmin_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, int32_t* x0lds,
                              BlockCounters* bc) {
@@ -218,18 +223,31 @@ PSG_DEV void floodmin_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_
       int32_t nx[W];
 #pragma unroll
       for (int j = 0; j < W; ++j) nx[j] = min(x[j], mU);
-      // crash round of some alive sender q: its message reaches p iff p's bit of q's survival
-      // words (Surv, sender-keyed): one readlane per crashing sender and slot word
-      if (many(CNa)) {
-        Surv<W> rs;
-        rs.prep(sc, k, CNa, P.lane);
-        Mask<W> rem = CNa;
-        for (int t = 0; t < rs.ncr; ++t) {
+      // crash round of some alive sender: its message reaches p iff p's survival bit.
+      // Survival word w of p's stream is half w & 1 of Philox call w / 2 (Sched::draw with
+      // drop = 0): the senders are taken by call, two 64-pid words at a time.
+#pragma unroll
+      for (int s = 0; 2 * s < W; ++s) {
+        Mask<W> rem = mzero<W>();
+        rem.w[2 * s] = CNa.w[2 * s];
+        if (2 * s + 1 < W) rem.w[2 * s + 1] = CNa.w[2 * s + 1];
+        if (!many(rem)) continue;
+        uint64_t h0[W], h1[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), (uint32_t)k,
+                                (uint32_t)P.pid(j) + ((uint32_t)s << 16), (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+          h0[j] = (uint64_t)o.x | ((uint64_t)o.y << 32);
+          h1[j] = (uint64_t)o.z | ((uint64_t)o.w << 32);
+        }
+        while (many(rem)) {
           const int q = mtake_first(rem);
           const int32_t xq = P.bcast(x, q);
+          const bool hi = (q >> 6) & 1;
+          const int qb = q & 63;
 #pragma unroll
           for (int j = 0; j < W; ++j)
-            if ((rs.word(sc, k, t, j, P.lane) >> P.lane) & 1ull) nx[j] = min(nx[j], xq);
+            if (((hi ? h1[j] : h0[j]) >> qb) & 1ull) nx[j] = min(nx[j], xq);
         }
       }
       const bool decideNow = a.variant == 1 ? (k >= f - 1) : (k > f);  // FloodMin.scala:27 (variant 1: mutation)
@@ -345,7 +363,7 @@ PSG_DEV void floodmin_body(const KArgs& a) {
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) cs.sets(g, k, CB, CN);
-        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, crash_drop<W>(sc, k, CN, g.wv, g.lane, g.lane)), act);
+        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         pt.mark(1);
         if (tracing<SH>(a) && !halted) hs = mpopc(M);
         // x = min(x, min{x_q : q in M}) by ascending distinct sender values

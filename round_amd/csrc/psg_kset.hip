@@ -218,8 +218,6 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
           CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
         }
       }
-      Surv<W> rs;  // crash-round survival words of this round's crashing senders (sender-keyed)
-      rs.prep(sc, k, CN, P.lane);
       uint32_t dw[W];
 #pragma unroll
       for (int j = 0; j < W; ++j) dw[j] = (fw >> j) & 1u;
@@ -330,7 +328,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
         uint32_t becomeDec = 0;
         const bool halted = halt_round[j] >= 0;  // before this round (set below when it decides)
         const uint32_t decider = (fw >> j) & 1u;
-        const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, rs.drop(sc, k, j, P.lane, P.lane)), act);
+        const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
         const uint32_t live = P.val[j] & (halted ? 0u : 1u) & (1u - decider);
         const uint32_t hc = many(mand(M, Dm)) ? 1u : 0u;
         const uint32_t adopt = live & hc, mergep = live & (1u - hc);
@@ -514,7 +512,7 @@ PSG_DEV void kset_body(const KArgs& a) {
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) cs.sets(g, k, CB, CN);
-        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, crash_drop<W>(sc, k, CN, g.wv, g.lane, g.lane)), act);
+        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         pt.mark(1);
         if (tracing<SH>(a) && !halted) hs = mpopc(M);
         const Mask<W> Dm = mand(g.ballot(decider), act);  // senders' decider flags (pre-state)

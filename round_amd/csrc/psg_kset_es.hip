@@ -86,14 +86,12 @@ PSG_DEV void kset_es_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t
           CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
         }
       }
-      Surv<W> rs;  // crash-round survival words of this round's crashing senders (sender-keyed)
-      rs.prep(sc, k, CN, P.lane);
       // The distinct sender estimates are visited in ascending order (the first step's value
       // is the minimum over every alive sender, known before any mailbox); each receiver
       // resolves at the first value whose senders meet its mailbox. A receiver's mailbox
       // (W words) is formed, used for the first step and dropped: the rare receivers still
       // unresolved after it re-form theirs at each later step (Sched::ho is a pure function
-      // of (k, pid) and this round's survival words), so no W x W
+      // of (k, pid); with crash-stop HO sets it draws only in the crash rounds), so no W x W
       // words of mailboxes stay live in registers (they spilled to scratch).
       int32_t mn = INT32_MAX;
 #pragma unroll
@@ -108,7 +106,7 @@ PSG_DEV void kset_es_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t
       uint32_t unres = 0, selfIn = 0, dnow = 0;  // bit j per slot
 #pragma unroll
       for (int j = 0; j < W; ++j) {
-        const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, rs.drop(sc, k, j, P.lane, P.lane)), act);
+        const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
         const int32_t currNb = mpopc(M);
         const uint32_t live = 1u - ((fl >> (8 + j)) & 1u);
         const uint32_t cd = (fl >> j) & 1u;
@@ -151,9 +149,8 @@ PSG_DEV void kset_es_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t
         rem = mandn(rem, E);
 #pragma unroll
         for (int j = 0; j < W; ++j) {
-          const Mask<W> CNd = rs.drop(sc, k, j, P.lane, P.lane);  // converged: readlanes of the crashing senders
           if ((unres >> j) & 1u) {
-            const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CNd), act);
+            const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
             if (many(mand(M, E))) {
               nest[j] = v;
               unres &= ~(1u << j);
@@ -266,7 +263,7 @@ PSG_DEV void kset_es_body(const KArgs& a) {
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) cs.sets(g, k, CB, CN);
-        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, crash_drop<W>(sc, k, CN, g.wv, g.lane, g.lane)), act);
+        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const int currNb = mpopc(M);
         if (!halted) hs = currNb;
         const bool anyCD = many(mand(M, m0[1]));  // mailbox.exists(_._2._2), pre-update flags

@@ -216,26 +216,27 @@ PSG_DEV Mask<W> ho_of(Grp<W>& g, LvLds<W>& L, const Mask<W>& ho, int c) {
 // same words and the same assembly as a per-lane Sched::ho).
 template <int W, bool XHO>
 struct CoordWords {
-  uint64_t dm[W];
+  uint64_t dm[W], hf[W];
   int qbase;
   PSG_DEV static int index(int k) { return (k >> 2) * 2 + ((k >> 1) & 1); }  // k even
   PSG_DEV void prep(const Sched<W, XHO>& sc, int q0, int lane, int n) {
     qbase = q0;
     const int q = q0 + lane;
     const int k = 4 * (q >> 1) + 2 * (q & 1);
-    sc.draw((uint32_t)k, (uint32_t)((k >> 2) % n), false, dm);
+    sc.draw((uint32_t)k, (uint32_t)((k >> 2) % n), false, sc.crash_on, dm, hf);
   }
-  // the crash-round survival bits of the coordinator (a uniform receiver) come from the
-  // crashing senders' words (sender-keyed, crash_drop), one readlane per crashing sender
-  PSG_DEV Mask<W> ho(const Sched<W, XHO>& sc, int k, int c, int lane, int n, bool good,
-                     const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CN) {
+  PSG_DEV Mask<W> ho(const Sched<W, XHO>& sc, int k, int c, int lane, int n, bool good, const Mask<W>& goodS,
+                     const Mask<W>& CB, const Mask<W>& CN) {
     const int q = index(k);
     if (q - qbase >= 64) prep(sc, q, lane, n);
     const int off = q - qbase;
-    uint64_t d[W];
+    uint64_t d[W], h[W];
 #pragma unroll
-    for (int w = 0; w < W; ++w) d[w] = readlane64(dm[w], off);
-    return sc.assemble(c, good, goodS, CB, crash_drop<W>(sc, k, CN, c >> 6, c & 63, lane), d);
+    for (int w = 0; w < W; ++w) {
+      d[w] = readlane64(dm[w], off);
+      h[w] = readlane64(hf[w], off);
+    }
+    return sc.assemble(c, good, goodS, CB, CN, d, h);
   }
 };
 
@@ -326,10 +327,10 @@ PSG_DEV void lv_body(const KArgs& a) {
           // only bit coord of HO(p) is read: the crash-round survival words matter only
           // when the coordinator crashes in this round, or when |HO(p)| decides the
           // ho_min rule (other bits are left unspecified otherwise)
-          uint64_t dm[W];
+          uint64_t dm[W], hf[W];
           const bool crash = sc.crash_on && (mtest(CN, c) || (sc.ho_min >= 0 && many(CN)));
-          sc.draw((uint32_t)k, (uint32_t)g.pid, good, dm);
-          HO = sc.assemble(g.pid, good, goodS, CB, crash ? crash_drop<W>(sc, k, CN, g.wv, g.lane, g.lane) : mzero<W>(), dm);
+          sc.draw((uint32_t)k, (uint32_t)g.pid, good, crash, dm, hf);
+          HO = sc.assemble(g.pid, good, goodS, CB, CN, dm, hf);
         }
         if constexpr (coordRound) {
           if constexpr (XHO) HOc = ho_of<W>(g, L, HO, c);

@@ -189,7 +189,7 @@ PSG_DEV void otr_body(const KArgs& a) {
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) cs.sets(g, k, CB, CN);
         // mailbox: broadcast(x) from every alive sender in HO(p)
-        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, crash_drop<W>(sc, k, CN, g.wv, g.lane, g.lane)), act);
+        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
         const int32_t msize = mpopc(M);
         if (tracing_on) hs = halted01 ? n : msize;
         const uint32_t upd = (1u - halted01) & gt01(msize, thr);

@@ -50,6 +50,21 @@ struct Pk {
   }
 };
 
+// First set pid of a non-empty mask, cleared from it (word-wise selects: a dynamic
+// word index would send the mask to scratch memory).
+template <int W>
+PSG_DEV int mtake_first(Mask<W>& a) {
+  int q = 0;
+  bool done = false;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const bool here = !done && a.w[i] != 0ull;
+    q = here ? i * 64 + (int)__builtin_ctzll(a.w[i]) : q;
+    a.w[i] = here ? a.w[i] & (a.w[i] - 1ull) : a.w[i];
+    done = done || here;
+  }
+  return q;
+}
 
 // Some lane's 0/1 word is set (uniform).
 PSG_DEV bool pk_any(uint32_t p) { return __builtin_amdgcn_ballot_w64(p != 0u) != 0ull; }

@@ -18,7 +18,6 @@ template <int W>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) schedule_kernel(KArgs a, uint64_t* ho_out, int32_t* crash_out) {
   __shared__ uint64_t xb[Grp<W>::kXb];
   __shared__ int64_t red[2 * W];
-  __shared__ int32_t crl[W > 1 ? 64 * W : 1];
   Grp<W> g;
   grp_setup(g, a, xb, red);
   constexpr int G = Geometry<W>::kGroups;
@@ -30,14 +29,15 @@ __global__ void __launch_bounds__(Geometry<W>::kThreads) schedule_kernel(KArgs a
     sc.setup(a, inst, g.pid, g.valid);
     sc.prep_good(0, g.lane, a.R);
     if (crash_out && g.valid) crash_out[i * (uint64_t)n + g.pid] = sc.crash_round;
-    CrashSets<W> cs;  // the same crash sets and survival words as the round kernels
-    if (sc.crash_on) cs.prep(g, crl, sc.crash_round);
     for (int k = 0; k < a.R; ++k) {
       Mask<W> goodS;
       const bool good = sc.good_round(k, g.lane, a.R, goodS);
       Mask<W> CB = mzero<W>(), CN = mzero<W>();
-      if (sc.crash_on) cs.sets(g, k, CB, CN);
-      const Mask<W> HO = sc.ho(k, g.pid, good, goodS, CB, crash_drop<W>(sc, k, CN, g.wv, g.lane, g.lane));
+      if (sc.crash_on) {
+        CB = g.ballot(sc.crash_round >= 0 && sc.crash_round < k);
+        CN = g.ballot(sc.crash_round == k);
+      }
+      const Mask<W> HO = sc.ho(k, g.pid, good, goodS, CB, CN);
       if (g.valid) {
         uint64_t* q = ho_out + ((i * (uint64_t)a.R + (uint64_t)k) * (uint64_t)n + (uint64_t)g.pid) * W;
 #pragma unroll

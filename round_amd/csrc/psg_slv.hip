@@ -128,7 +128,7 @@ PSG_DEV void slv_body(const KArgs& a) {
         // (ShortLastVoting.scala:53): the other rounds' and silent R1s' draws are skipped
         const bool sent = RS == 1 && cAlive && mtest(g.ballot((fl & S_COMMIT) != 0u), c);
         Mask<W> HO = mzero<W>();
-        if (RS != 1 || sent) HO = sc.ho(k, g.pid, good, goodS, CB, crash_drop<W>(sc, k, CN, g.wv, g.lane, g.lane));
+        if (RS != 1 || sent) HO = sc.ho(k, g.pid, good, goodS, CB, CN);
         if constexpr (W > 1) {
           L.xs[g.pid] = x;
           L.votes[g.pid] = vote;
