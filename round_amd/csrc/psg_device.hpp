@@ -123,7 +123,7 @@ enum { C_FAIL = 0, C_DECIDED = PSG_MAX_CHECKS, C_DIGEST = PSG_MAX_CHECKS + 1,
        // then (start, end) per wave for the first 16384 waves)
        // instance queues (InstanceQueue): NQUEUES counters, one per 128 B line
        C_QUEUE = NCOUNTERS, NQUEUES = 8, QUEUE_STRIDE = 16,
-       C_TIMER = C_QUEUE + NQUEUES * QUEUE_STRIDE, NTIMERS = 6, NSTAMP_WAVES = 16384,
+       C_TIMER = C_QUEUE + NQUEUES * QUEUE_STRIDE, NTIMERS = 8, NSTAMP_WAVES = 16384,
        T_RT_SUM = NTIMERS, T_RT_MIN = NTIMERS + 1, T_RT_MAX = NTIMERS + 2, T_WAVES = NTIMERS + 3,
        T_STAMPS = NTIMERS + 4,
        NTIMER_SLOTS = PSG_PHASE_TIMERS ? T_STAMPS + 2 * NSTAMP_WAVES : 0, NCOUNTERS_ALLOC = C_TIMER + NTIMER_SLOTS };
@@ -139,10 +139,14 @@ struct PhaseTimers {
     last = __builtin_amdgcn_s_memtime();
   }
   PSG_DEV void mark(int j) {
+#if PSG_PHASE_TIMERS == 1
     const uint64_t t = __builtin_amdgcn_s_memtime();
     acc[j] += t - last;
     last = t;
+#endif
   }
+  // event-count builds (-DPSG_PHASE_TIMERS=2): mark() is off, the slots count events instead
+  PSG_DEV void add(int j, uint64_t v) { acc[j] += v; }
   PSG_DEV void flush(unsigned long long* g, int lane) {
     const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
@@ -161,6 +165,7 @@ struct PhaseTimers {
 #else
   PSG_DEV void start() {}
   PSG_DEV void mark(int) {}
+  PSG_DEV void add(int, uint64_t) {}
   PSG_DEV void flush(unsigned long long*, int) {}
 #endif
 };
@@ -290,6 +295,11 @@ PSG_DEV uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 PSG_DEV uint64_t proc_digest(int pid, int32_t dec, int32_t dround, int32_t hround, int32_t mainx) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // opaque copy: the pid term is recomputed per instance instead of hoisted out of the instance
+  // loop and kept live (spilled to scratch) across every round
+  asm volatile("" : "+v"(pid));
+#endif
   uint64_t y = ((uint64_t)(uint32_t)pid << 32) | ((uint64_t)((uint32_t)dround & 0xFFFFu) << 16) |
                (uint64_t)((uint32_t)hround & 0xFFFFu);
   uint64_t z = ((uint64_t)(uint32_t)dec << 32) | (uint64_t)(uint32_t)mainx;
@@ -949,16 +959,34 @@ struct Sched {
   // is the crash-round survival mask hf[w] of word w. good: the drop words are not
   // needed (the round's common set replaces them); crash = false: the survival
   // words are not needed (no process crashes in round k) and hf stays all-ones.
-  PSG_DEV void draw(uint32_t k, uint32_t pid, bool good, bool crash, uint64_t (&dm)[W], uint64_t (&hf)[W]) const {
+  // cw (uniform): bit w set iff survival word w is needed (some process of pid word w crashes in
+  // round k); a call whose two words are neither drop words nor needed survival words is skipped
+  // (those survival words are only ever ANDed with an empty CN word: packed KSet at n = 256
+  // draws one call instead of two in most crash rounds).
+  PSG_DEV void draw(uint32_t k, uint32_t pid, bool good, bool crash, uint64_t (&dm)[W], uint64_t (&hf)[W],
+                    uint32_t cw = ~0u) const {
     const uint32_t nd = (uint32_t)W * drop;
     const uint32_t j0 = good ? nd : 0u;
+#ifdef PSG_ABL_CHEAP_SURV
+    const uint32_t j1 = good ? 0u : nd;
+#else
     const uint32_t j1 = crash ? nd + (uint32_t)W : (good ? 0u : nd);
+#endif
 #pragma unroll
     for (int w = 0; w < W; ++w) {
       dm[w] = ~0ull;
       hf[w] = ~0ull;
     }
     for (uint32_t sidx = j0 >> 1; 2 * sidx < j1; ++sidx) {
+      if constexpr (W > 1) {
+        bool need = false;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t j = 2 * sidx + (uint32_t)h;
+          need = need || (j >= j0 && j < j1 && (j < nd || ((cw >> (j - nd)) & 1u)));
+        }
+        if (!need) continue;
+      }
       const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), k, pid + (sidx << 16), (uint32_t)seed,
                             (uint32_t)(seed >> 32));
       const uint64_t wlo = (uint64_t)o.x | ((uint64_t)o.y << 32);
@@ -980,6 +1008,15 @@ struct Sched {
         }
       }
     }
+#ifdef PSG_ABL_CHEAP_SURV  // probe builds only (wrong results): survival words without Philox
+    if (crash) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const uint64_t x = (inst ^ ((uint64_t)k << 40) ^ ((uint64_t)pid << 20) ^ (uint64_t)w) * 0x9E3779B97F4A7C15ull;
+        hf[w] = x ^ (x >> 29);
+      }
+    }
+#endif
   }
 
   // HO(pid) from its raw words. CB = processes crashed before round k, CN =
@@ -1009,7 +1046,10 @@ struct Sched {
       return m;
     }
     uint64_t dm[W], hf[W];
-    draw((uint32_t)k, (uint32_t)pid, good, crash_on && many(CN), dm, hf);
+    uint32_t cw = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) cw |= CN.w[w] ? 1u << w : 0u;
+    draw((uint32_t)k, (uint32_t)pid, good, crash_on && cw != 0u, dm, hf, cw);
     return assemble(pid, good, goodS, CB, CN, dm, hf);
   }
 };
@@ -1127,7 +1167,7 @@ PSG_DEV void finish_instance(Grp<W>& g, const KArgs& a, uint64_t i, const Checks
                              StepTally* tally = nullptr, int32_t live_rounds = -1) {
   const int n = a.n;
   const bool decided = dec_round >= 0;
-const uint64_t d = g.valid ? proc_digest(g.pid, dec_val, dec_round, halt_round, main_x) : 0ull;
+  const uint64_t d = g.valid ? proc_digest(g.pid, dec_val, dec_round, halt_round, main_x) : 0ull;
   const uint64_t dig = g.sum64(d);
   const int nd = mpopc(g.ballot(decided));
   // rounds in which this process took a step: up to and including its halting round

@@ -121,7 +121,10 @@ PSG_DEV void floodmin_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashS
       int32_t nx = min(x, mU);
       if (many(CNa)) {  // crash round of some alive sender: its message reaches p iff p's survival bit
         uint64_t dm[W], hf[W];
-        sc.draw((uint32_t)k, (uint32_t)g.pid, false, true, dm, hf);
+        uint32_t cw = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) cw |= CNa.w[w] ? 1u << w : 0u;
+        sc.draw((uint32_t)k, (uint32_t)g.pid, false, true, dm, hf, cw);
         Mask<W> rem = CNa;
         while (many(rem)) {
           const int q = mfirst(rem);

@@ -192,7 +192,9 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
       decided[j] = halt_round[j] >= 0 ? 1u : 0u;
       notinit[j] = (fw >> (8 + j)) & 1u;
     }
+#ifndef PSG_ABL_NOCHECK  // probe builds only (wrong results): check points skipped
     pk_kagree_check_m<W>(P, ck, c, kk, decided, decision, cr, notinit);
+#endif
   };
   check(0);
   pt.mark(0);
@@ -322,6 +324,14 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
         lds_sync<1>();
       }
       pt.mark(1);
+      pt.add(0, 1);  // event-count builds: round paths (live, closed, uniform t, columns, classes)
+      pt.add(1, closed);
+      pt.add(2, cols && ncols == 0);
+      pt.add(3, cols && ncols > 0);
+      pt.add(4, cols ? ncols : 0);
+      pt.add(5, !closed && !cols);
+      pt.add(6, !closed && !cols ? mpopc(rem) : 0);
+      pt.add(7, many(CN));
       // one slot at a time (its HO set M, its merge or adoption)
 #pragma unroll
       for (int j = 0; j < W; ++j) {

@@ -1,5 +1,5 @@
 """A/B probe of the headline launch (OTR n=64, 1e7 instances, R=20, V=64 and V=2; arg lv: C3 LastVoting;
-kset: the C4 KSet rows at f = 1, 16, 64):
+kset: the C4 KSet rows at f = 1, 16, 64; fm, kses, benor, slv, eps: the C4 / C5 / W2 rows):
 min kernel ms over 5 launches for the library PSG_LIB points at (default: in-tree)."""
 import os
 import sys
@@ -20,10 +20,14 @@ elif which == "kses":  # W2 KSetEarlyStopping: n=256, t=64, k=2, 1e6 instances, 
     runs = [(psync.KSetEarlyStopping(64, 2), 1_000_000, {}, "KSetES W2")]
 elif which == "benor":  # C5: BenOr n=128, 1e6 instances, R=64
     runs = [(psync.BenOr(), 1_000_000, {}, "BenOr C5")]
+elif which == "slv":  # W2 ShortLastVoting: n=64, 1.25e7 instances, default rounds / schedule
+    runs = [(psync.ShortLastVoting(), 12_500_000, {}, "SLV W2")]
+elif which == "eps":  # W2 EpsilonConsensus: n=64, f=5, 1e6 instances, default rounds / schedule
+    runs = [(psync.EpsilonConsensus(5, 1e-6), 1_000_000, {}, "Epsilon W2")]
 else:  # BASELINE C3 shard: LastVoting n=64, 1.25e7 instances, crash-stop
     runs = [(psync.LastVoting(), 12_500_000, {}, "LV C3")]
 for alg, I, kw, label in runs:
-    n, R = {"kset": (256, 16), "fm": (256, None), "kses": (256, None), "benor": (128, 64)}.get(
+    n, R = {"kset": (256, 16), "fm": (256, None), "kses": (256, None), "benor": (128, 64), "slv": (64, None), "eps": (64, None)}.get(
         which, (64, 20))  # None: the algorithm's default rounds
     with psync.GpuRound(alg, n, R, seed=2, batch_capacity=I, **kw) as g:
         g.load_inputs(0, I)
