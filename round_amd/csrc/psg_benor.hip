@@ -399,7 +399,7 @@ PSG_DEV void benor_body(const KArgs& a) {
     if (sc.crash_on) cs.prep(g, crl, sc.crash_round);
     sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
-    if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_BENOR);
+    if (g.valid) x0 = a.init ? init_x(a, i, inst, g.pid) : sc.init_value(g.pid, PSG_ALG_BENOR);
     if constexpr (!SH::kFused) {
       if (a.trace == nullptr) {  // built-in checker: one exchange per round
         benor_fast<W>(g, a, i, sc, cs, BX, x0, &bc);

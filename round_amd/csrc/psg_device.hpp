@@ -73,6 +73,14 @@ struct KArgs {
 // Initial value of process pid of batch element i (global id inst): staged rows
 // are indexed by batch position, or by global id in the fetch (ids) path.
 PSG_DEV uint64_t init_row(const KArgs& a, uint64_t i, uint64_t inst) { return a.ids ? inst - a.init_base : i; }
+// Host-supplied initial value of process pid (a.init non-null). The pid term of the address is
+// formed here per instance (opaque copy), not hoisted out of the instance loop and kept live.
+PSG_DEV int32_t init_x(const KArgs& a, uint64_t i, uint64_t inst, int pid) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(pid));
+#endif
+  return a.init[init_row(a, i, inst) * (uint64_t)a.n + (uint64_t)pid];
+}
 
 // Spec-program interpreter arguments (psg_spec_vm.hip)
 struct VmArgs {
@@ -1508,7 +1516,13 @@ PSG_DEV int32_t maxby_ts_x(Grp<W>& g, const int32_t* xs, const Mask<W>& Mc, int 
   int win = q0;
   const bool differ = many(mand(T, g.ballot(x != xq0)));
   if (differ && tiebreak == PSG_TIE_CHAMP && size > 4) {
-    // payload depth of each candidate = longest 5-bit hash prefix shared with another entry
+    // payload depth of each candidate = longest 5-bit hash prefix shared with another entry.
+    // h: an opaque copy of the lane's hash, so the fragment values derived from it are formed in
+    // this (rare) block instead of hoisted out of the kernel's loops and held live
+    uint32_t h = myh;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(h));
+#endif
     int depth = 0;
     if (CT) {
       // per lane, level by level: the entries sharing this lane's first l+1 fragments are the
@@ -1518,7 +1532,7 @@ PSG_DEV int32_t maxby_ts_x(Grp<W>& g, const int32_t* xs, const Mask<W>& Mc, int 
       Mask<W> S = Mc;
 #pragma unroll
       for (int l = 0; l < 7; ++l) {
-        const uint32_t f = (myh >> (5 * l)) & 31u;
+        const uint32_t f = (h >> (5 * l)) & 31u;
 #pragma unroll
         for (int w = 0; w < W; ++w) S.w[w] &= CT->b[l][f][w];
         depth += mpopc(S) >= 2 ? 1 : 0;
@@ -1530,12 +1544,12 @@ PSG_DEV int32_t maxby_ts_x(Grp<W>& g, const int32_t* xs, const Mask<W>& Mc, int 
         while (m) {
           const int f = w * 64 + __builtin_ctzll(m);
           m &= m - 1;
-          if (f != g.pid) depth = max(depth, champ_cpl(myh, scala_improve((uint32_t)f)));
+          if (f != g.pid) depth = max(depth, champ_cpl(h, scala_improve((uint32_t)f)));
         }
       }
     }
     const bool inT = mtest(T, g.pid);
-    const int64_t key = (int64_t)champ_key(myh, depth);
+    const int64_t key = (int64_t)champ_key(h, depth);
     const int64_t kmin = g.min64(key, inT);
     win = mfirst(mand(T, g.ballot(key == kmin)));
   }

@@ -183,7 +183,7 @@ PSG_DEV void floodmin_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_
   for (int j = 0; j < W; ++j) {
     x[j] = 0;
     if (P.val[j])
-      x[j] = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + P.pid(j)] : sc.init_value(P.pid(j), PSG_ALG_FLOODMIN);
+      x[j] = a.init ? init_x(a, i, inst, P.pid(j)) : sc.init_value(P.pid(j), PSG_ALG_FLOODMIN);
   }
   X0Set<W> X0;
   pk_x0_build<W>(P, X0, x0lds, x);
@@ -323,7 +323,7 @@ PSG_DEV void floodmin_body(const KArgs& a) {
     sc.prep_good(0, g.lane, a.R);
     const bool crashed = sc.crash_round >= 0;
     int32_t x0 = 0;
-    if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_FLOODMIN);
+    if (g.valid) x0 = a.init ? init_x(a, i, inst, g.pid) : sc.init_value(g.pid, PSG_ALG_FLOODMIN);
     X0Set<W> X0;
     X0.build(g, x0tab[grp], x0);
     if constexpr (!XHO && !SH::kFused) {

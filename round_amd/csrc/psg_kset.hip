@@ -167,7 +167,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
   for (int j = 0; j < W; ++j) {
     x0[j] = 0;
     if (P.val[j])
-      x0[j] = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + P.pid(j)] : sc.init_value(P.pid(j), PSG_ALG_KSET);
+      x0[j] = a.init ? init_x(a, i, inst, P.pid(j)) : sc.init_value(P.pid(j), PSG_ALG_KSET);
     L.x0s[P.pid(j)] = x0[j];
     if (P.val[j]) xmin_l = min(xmin_l, x0[j]);
     // t = Map(id -> io.initialValue); decider = false (KSetAgreement.scala:27-31)
@@ -489,7 +489,7 @@ PSG_DEV void kset_body(const KArgs& a) {
     sc.prep_good(0, g.lane, a.R);
     const bool crashed = sc.crash_round >= 0;
     int32_t x0 = 0;
-    if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_KSET);
+    if (g.valid) x0 = a.init ? init_x(a, i, inst, g.pid) : sc.init_value(g.pid, PSG_ALG_KSET);
     x0s[g.pid] = x0;
     X0Set<W> X0;
     X0.build(g, x0tab[grp], x0);

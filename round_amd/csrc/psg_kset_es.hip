@@ -47,7 +47,7 @@ PSG_DEV void kset_es_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t
   for (int j = 0; j < W; ++j) {
     est[j] = 0;
     if (P.val[j])
-      est[j] = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + P.pid(j)] : sc.init_value(P.pid(j), PSG_ALG_KSET_ES);
+      est[j] = a.init ? init_x(a, i, inst, P.pid(j)) : sc.init_value(P.pid(j), PSG_ALG_KSET_ES);
     nbh[j] = (uint32_t)n;
     decision[j] = 0;
     fl |= (1u - P.val[j]) << (8 + j);
@@ -229,7 +229,7 @@ PSG_DEV void kset_es_body(const KArgs& a) {
     sc.prep_good(0, g.lane, a.R);
     const bool crashed = sc.crash_round >= 0;
     int32_t x0 = 0;
-    if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_KSET_ES);
+    if (g.valid) x0 = a.init ? init_x(a, i, inst, g.pid) : sc.init_value(g.pid, PSG_ALG_KSET_ES);
     X0Set<W> X0;
     X0.build(g, x0tab[grp], x0);
     // KSetESProcess state after init(io) (KSetEarlyStopping.scala:16-21)

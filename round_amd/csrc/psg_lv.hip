@@ -277,7 +277,7 @@ PSG_DEV void lv_body(const KArgs& a) {
     CoordWords<W, XHO> cw;
     if constexpr (!XHO) cw.prep(sc, 0, g.lane, n);
     int32_t x0 = 0;
-    if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_LAST_VOTING);
+    if (g.valid) x0 = a.init ? init_x(a, i, inst, g.pid) : sc.init_value(g.pid, PSG_ALG_LAST_VOTING);
     X0Set<W> X0;
     X0.build(g, x0tab[grp], x0);
     // LVProcess state after init(io) (LastVoting.scala:82-109)

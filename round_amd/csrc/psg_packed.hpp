@@ -126,15 +126,43 @@ PSG_DEV void pk_kagree_check_m(const Pk<W>& P, Checks& ck, int c, int kk, const 
     undec |= P.val[j] & (1u - decided[j]);
     bad |= P.val[j] & decided[j] & notinit[j];
   }
-  Mask<W> Y = P.ballot(dc);
-  int distinct = 0;
-  while (many(Y) && distinct <= kk) {
-    const int32_t dv = P.bcast(decision, mfirst(Y));
-    uint32_t eq[W];
+  // |distinct decisions| from the deciders' min and max (two independent DPP reductions, no
+  // scalar walk): none (mn > mx), one (mn == mx), or two plus a ballot for a third value; only
+  // k >= 3 with a third value walks the values one by one
+  uint32_t anyd = 0;
+  int32_t lmn = INT32_MAX, lmx = INT32_MIN;
 #pragma unroll
-    for (int j = 0; j < W; ++j) eq[j] = dc[j] & eq01(decision[j], dv);
-    Y = mandn(Y, P.ballot(eq));
-    ++distinct;
+  for (int j = 0; j < W; ++j) {
+    anyd |= dc[j];
+    lmn = dc[j] ? min(lmn, decision[j]) : lmn;
+    lmx = dc[j] ? max(lmx, decision[j]) : lmx;
+  }
+  int distinct = 0;
+  int32_t mn = 0, mx = 0;
+  if (pk_any(anyd)) {  // (no correct decider: one ballot)
+    mn = Grp<1>::dpp_reduce32<false>(lmn);
+    mx = Grp<1>::dpp_reduce32<true>(lmx);
+    distinct = mn == mx ? 1 : 2;
+  }
+  if (distinct == 2 && kk >= 2) {
+    uint32_t third = 0;
+#pragma unroll
+    for (int j = 0; j < W; ++j) third |= dc[j] & ne01(decision[j], mn) & ne01(decision[j], mx);
+    if (pk_any(third)) {
+      distinct = 3;
+      if (kk >= 3) {  // the general walk: one value per step, stopping past k
+        Mask<W> Y = P.ballot(dc);
+        distinct = 0;
+        while (many(Y) && distinct <= kk) {
+          const int32_t dv = P.bcast(decision, mfirst(Y));
+          uint32_t eq[W];
+#pragma unroll
+          for (int j = 0; j < W; ++j) eq[j] = dc[j] & eq01(decision[j], dv);
+          Y = mandn(Y, P.ballot(eq));
+          ++distinct;
+        }
+      }
+    }
   }
   ck.record(fbit(distinct <= kk, 0) | fbit(!pk_any(bad), 1), !pk_any(undec), c, P.lane);
 }

@@ -86,7 +86,7 @@ PSG_DEV void slv_body(const KArgs& a) {
     if (sc.crash_on) cs.prep(g, crl, sc.crash_round);
     sc.prep_good(0, g.lane, a.R);
     int32_t x0 = 0;
-    if (g.valid) x0 = a.init ? a.init[init_row(a, i, inst) * (uint64_t)n + g.pid] : sc.init_value(g.pid, PSG_ALG_SLV);
+    if (g.valid) x0 = a.init ? init_x(a, i, inst, g.pid) : sc.init_value(g.pid, PSG_ALG_SLV);
     X0Set<W> X0;
     X0.build(g, x0tab[grp], x0);
     // SlvProcess state after init(io) (ShortLastVoting.scala:15-31)

@@ -173,3 +173,9 @@ def test_lowering_shapes_in_source():
     assert "quant_tup" in plain and "tup_uniform_g" not in plain and "tup_uniform<" in plain
     assert "spec::uniform<" in plain and "spec::uniform<" not in src(
         P.exists(lambda i: P.forall(lambda j: j.decided & (j.decision == i.x))), options=["nosym"])
+    # V.exists finitization: order comparisons on the breakpoints, == / != on the candidates plus
+    # one outside value, a pinned variable at its pin (exactness: test_gpu_spec, all three modes)
+    V = F.V
+    assert "spec::exists_int_bp<" in src(V.exists(lambda v: P.forall(lambda i: i.x <= v)))
+    assert "spec::exists_int_eq<" in src(V.exists(lambda v: P.forall(lambda i: i.x == v)))
+    assert "spec::exists_int_pin<" in src(V.exists(lambda v: P.forall(lambda i: i.decided.implies(i.decision == v))))
