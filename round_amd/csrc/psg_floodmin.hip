@@ -167,7 +167,7 @@ PSG_DEV void floodmin_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashS
 template <int W>
 PSG_DEV void floodmin_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, int32_t* x0lds,
                              BlockCounters* bc) {
-  const int n = a.n, f = a.param;
+  const int f = a.param;
   Sched<W, false> sc;
   sc.setup(a, inst, P.lane, false);  // uniform parts; crash rounds per slot below
   int32_t cr[W];
