@@ -200,12 +200,17 @@ PSG_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // v_mul_hi_u32 pair measured 7 % slower per call, scripts/mb_philox.hip; the headline -1.4 %).
 // Round 0's products stay in C: their operands are often wave-uniform (scalar multiplies).
 #ifndef PSG_PHILOX_MAD64
-#define PSG_PHILOX_MAD64 1
+#define PSG_PHILOX_MAD64 2  // 2: carry-out in VCC (no SGPR pair per product: fused OTR -1.8 %, gpu_probe_r4r.sh)
 #endif
 #if PSG_PHILOX_MAD64 && defined(__HIP_DEVICE_COMPILE__)
 PSG_DEV uint64_t mul64_mad(uint32_t a, uint32_t b) {
-  uint64_t r, cy;
+  uint64_t r;
+#if PSG_PHILOX_MAD64 == 2  // carry-out into VCC (clobbered): no SGPR pair allocated per product
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b) : "vcc");
+#else
+  uint64_t cy;
   asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cy) : "v"(a), "v"(b));
+#endif
   return r;
 }
 #define PSG_MUL64(r, a, b) ((r) == 0 ? (uint64_t)(a) * (b) : mul64_mad((a), (b)))
@@ -1107,8 +1112,11 @@ struct Checks {
   PSG_DEV void reset() { ffv = PSG_NEVER; }
   // failbits: bit s set iff slot s is false at check point c (uniform); term: Termination holds
   PSG_DEV void record(uint32_t failbits, bool term, int c, int lane) {
-    const uint64_t bits = (uint64_t)(failbits | (term ? (1u << PSG_MAX_CHECKS) : 0u));
-    const int32_t at = ((bits >> lane) & 1ull) ? c : (int32_t)PSG_NEVER;  // lane < 64: a defined shift
+    const uint32_t bits = failbits | (term ? (1u << PSG_MAX_CHECKS) : 0u);
+    // lane's bit of the 13-bit word (a 32-bit shift reads only the amount's low 5 bits: lanes
+    // past PSG_MAX_CHECKS take the all-zero mask instead, one AND + compare per check point)
+    const uint32_t mine = lane <= PSG_MAX_CHECKS ? 1u << lane : 0u;
+    const int32_t at = (bits & mine) ? c : (int32_t)PSG_NEVER;
     ffv = at < ffv ? at : ffv;
   }
   // slot `lane` (< PSG_MAX_CHECKS) failed at some check point

@@ -37,10 +37,12 @@ struct OtrLds {
 // slower, profiles/s2_ab/ab5.log: the chain's latency; a compare + ballot has none.)
 // V.exists(v => |{i : i.x == v}| > 2n/3 && all decisions == v): with decisions only
 // v = d0 can qualify; without, v must be a strict majority (Boyer-Moore candidate).
-template <int W, bool V2>
+template <int W, bool V2, bool FROZEN = false>
 // od / ox: "decision / x maybe not initial" (X0Set::maybe_out01_2 of the current values), probed
 // by the caller when the values change (round 0 and executed updates) instead of at every check
 // point: the memoized probe of the fused lowering; every formula is still evaluated.
+// FROZEN: a check point of the frozen tail, where the pre-round state is the current one, so the
+// Irrevocability witness old.decided && !(decided && old.decision == decision) is 0 by algebra.
 PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, int c, bool has_old, int n,
                        const Mask<W>& full, int32_t x, uint32_t dec01, int32_t decision, uint32_t old01,
                        int32_t old_decision, uint32_t valid01, uint32_t od, uint32_t ox) {
@@ -49,7 +51,7 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
     L.ds[g.pid] = decision;
     __syncthreads();
   }
-  const uint32_t irr01 = has_old ? old01 & (1u - (dec01 & eq01(old_decision, decision))) : 0u;
+  const uint32_t irr01 = (has_old && !FROZEN) ? old01 & (1u - (dec01 & eq01(old_decision, decision))) : 0u;
   {
     // Settled state first (every process decided, every decision equal to process 0's, no
     // witness): one ballot of a per-process word, with process 0's decision as d0 (when all
@@ -271,7 +273,7 @@ PSG_DEV void otr_body(const KArgs& a) {
     // these check points, kf + 1 .. R (Otr.scala:95-120 over the frozen state).
     for (int k = kf; k < a.R; ++k) {
       if constexpr (!SH::kFused)
-        otr_check<W, V2>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, dec01, decision, valid01, od, ox);
+        otr_check<W, V2, true>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, dec01, decision, valid01, od, ox);
       if (tracing_on) trace(k + 1, n);
       pt.mark(2);
     }

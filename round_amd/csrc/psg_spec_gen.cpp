@@ -1223,7 +1223,9 @@ std::string module_source(ParsedSpec& P, const Compiled& prog, int alg, bool fus
     std::vector<int> waves;
     if (n > 0) waves.push_back((n + 63) / 64);
     else waves = {1, 2, 3, 4};
-    src = "#define PSG_FUSED_MODULE 1\n" + src + fused_source(alg, waves);
+    // the compiler's mul_lo / mul_hi Philox products: the inline v_mad_u64_u32 form that wins in the
+    // library's round kernels measured 4-6 % slower in the fused modules (scripts/gpu_probe_r4r.sh)
+    src = "#define PSG_FUSED_MODULE 1\n#ifndef PSG_PHILOX_MAD64\n#define PSG_PHILOX_MAD64 0\n#endif\n" + src + fused_source(alg, waves);
   }
   return src;
 }
