@@ -143,7 +143,7 @@ PSG_DEV void benor_fast(Grp<W>& g, const KArgs& a, uint64_t i, SC& sc, CrashSets
       const bool good = sc.good_round(k, g.lane, a.R, goodS);
       Mask<W> CB = mzero<W>(), CN = mzero<W>();
       if (sc.crash_on) cs.sets(g, k, CB, CN);
-      const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+      const Mask<W> M = mand(sc.template ho<false>(k, g.pid, good, goodS, CB, CN), act);
       const int size = mpopc(M);
       predw = !halted && size <= n / 2;
       if ((k & 1) == 0) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
@@ -300,7 +300,7 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
 #pragma unroll
       for (int j = 0; j < W; ++j) {
         if (halted[j]) continue;  // a halted process neither receives nor updates
-        const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
+        const Mask<W> M = mand(sc.template ho<false>(k, P.pid(j), good, goodS, CB, CN), act);
         const int size = mpopc(M);
         predw[j] = P.val[j] & (size <= n / 2 ? 1u : 0u);
         if constexpr (even) {  // R0: broadcast (x, canDecide) — BenOr.scala:31-53
@@ -348,7 +348,7 @@ PSG_DEV void benor_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t i
   int32_t fx[W];
 #pragma unroll
   for (int j = 0; j < W; ++j) fx[j] = (int32_t)x[j];
-  pk_finish<W>(P, a, i, ck, 5, dec_val, dec_round, halt_round, fx, bc);
+  pk_finish<W, false>(P, a, i, ck, 5, dec_val, dec_round, halt_round, fx, bc);
 }
 
 #ifndef PSG_BO_PK_WPE
@@ -431,7 +431,7 @@ PSG_DEV void benor_body(const KArgs& a) {
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
         if (sc.crash_on) cs.sets(g, k, CB, CN);
-        const Mask<W> M = mand(sc.ho(k, g.pid, good, goodS, CB, CN), act);
+        const Mask<W> M = mand(sc.template ho<false>(k, g.pid, good, goodS, CB, CN), act);
         const int size = mpopc(M);
         pt.mark(1);
         if (!halted) hs = size;

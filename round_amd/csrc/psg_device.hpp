@@ -199,6 +199,9 @@ PSG_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // Philox's 32x32 -> 64-bit products as one v_mad_u64_u32 each (the compiler's v_mul_lo_u32 +
 // v_mul_hi_u32 pair measured 7 % slower per call, scripts/mb_philox.hip; the headline -1.4 %).
 // Round 0's products stay in C: their operands are often wave-uniform (scalar multiplies).
+#ifndef PSG_AB_NO_CW
+#define PSG_AB_NO_CW 0  // A/B builds only: 1 = no survival-call skip
+#endif
 #ifndef PSG_PHILOX_MAD64
 #define PSG_PHILOX_MAD64 2  // 2: carry-out in VCC (no SGPR pair per product: fused OTR -1.8 %, gpu_probe_r4r.sh)
 #endif
@@ -307,11 +310,13 @@ PSG_DEV uint64_t splitmix64(uint64_t x) {
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
   return x ^ (x >> 31);
 }
+template <bool OPAQUE = true>
 PSG_DEV uint64_t proc_digest(int pid, int32_t dec, int32_t dround, int32_t hround, int32_t mainx) {
 #if defined(__HIP_DEVICE_COMPILE__)
   // opaque copy: the pid term is recomputed per instance instead of hoisted out of the instance
-  // loop and kept live (spilled to scratch) across every round
-  asm volatile("" : "+v"(pid));
+  // loop and kept live (spilled to scratch) across every round (packed KSet's 12 B of scratch,
+  // FloodMin -2..5 %); packed BenOr keeps the hoisted form (3.6 % faster, gpu_probe_r4v.sh)
+  if constexpr (OPAQUE) asm volatile("" : "+v"(pid));
 #endif
   uint64_t y = ((uint64_t)(uint32_t)pid << 32) | ((uint64_t)((uint32_t)dround & 0xFFFFu) << 16) |
                (uint64_t)((uint32_t)hround & 0xFFFFu);
@@ -976,22 +981,13 @@ struct Sched {
   // round k); a call whose two words are neither drop words nor needed survival words is skipped
   // (those survival words are only ever ANDed with an empty CN word: packed KSet at n = 256
   // draws one call instead of two in most crash rounds).
-  PSG_DEV void draw(uint32_t k, uint32_t pid, bool good, bool crash, uint64_t (&dm)[W], uint64_t (&hf)[W],
-                    uint32_t cw = ~0u) const {
-    const uint32_t nd = (uint32_t)W * drop;
-    const uint32_t j0 = good ? nd : 0u;
-#ifdef PSG_ABL_CHEAP_SURV
-    const uint32_t j1 = good ? 0u : nd;
-#else
-    const uint32_t j1 = crash ? nd + (uint32_t)W : (good ? 0u : nd);
-#endif
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      dm[w] = ~0ull;
-      hf[w] = ~0ull;
-    }
+  // Words j0 .. j1 - 1 of pid's stream in round k into dm / hf; SKIP: a call whose two words are
+  // neither drop words nor survival words of a non-empty CN word (cw) is skipped.
+  template <bool SKIP>
+  PSG_DEV void draw_words(uint32_t k, uint32_t pid, uint32_t j0, uint32_t j1, uint32_t nd, uint32_t cw,
+                          uint64_t (&dm)[W], uint64_t (&hf)[W]) const {
     for (uint32_t sidx = j0 >> 1; 2 * sidx < j1; ++sidx) {
-      if constexpr (W > 1) {
+      if constexpr (SKIP) {
         bool need = false;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1021,6 +1017,27 @@ struct Sched {
         }
       }
     }
+  }
+  // SKIP = false: the plain loop (BenOr: the skip test in every call measured 9 % slower on its
+  // crash-free C5 rows, a skip-only-in-crash-rounds second loop 2.5 % slower on packed KSet;
+  // scripts/gpu_probe_r4v.sh, r4w)
+  template <bool SKIP = true>
+  PSG_DEV void draw(uint32_t k, uint32_t pid, bool good, bool crash, uint64_t (&dm)[W], uint64_t (&hf)[W],
+                    uint32_t cw = ~0u) const {
+    const uint32_t nd = (uint32_t)W * drop;
+    const uint32_t j0 = good ? nd : 0u;
+#ifdef PSG_ABL_CHEAP_SURV
+    const uint32_t j1 = good ? 0u : nd;
+#else
+    const uint32_t j1 = crash ? nd + (uint32_t)W : (good ? 0u : nd);
+#endif
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      dm[w] = ~0ull;
+      hf[w] = ~0ull;
+    }
+    constexpr bool kSkip = SKIP && W > 1 && !PSG_AB_NO_CW;
+    draw_words<kSkip>(k, pid, j0, j1, nd, cw, dm, hf);
 #ifdef PSG_ABL_CHEAP_SURV  // probe builds only (wrong results): survival words without Philox
     if (crash) {
 #pragma unroll
@@ -1048,6 +1065,7 @@ struct Sched {
   }
 
   // HO(p) for this lane's process p in round k.
+  template <bool SKIP = true>
   PSG_DEV Mask<W> ho(int k, int pid, bool good, const Mask<W>& goodS, const Mask<W>& CB, const Mask<W>& CN) const {
     if constexpr (XHO) {  // explicit: W contiguous words per process, the wave reads 512*W contiguous bytes
       Mask<W> m = mzero<W>();
@@ -1062,7 +1080,7 @@ struct Sched {
     uint32_t cw = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) cw |= CN.w[w] ? 1u << w : 0u;
-    draw((uint32_t)k, (uint32_t)pid, good, crash_on && cw != 0u, dm, hf, cw);
+    draw<SKIP>((uint32_t)k, (uint32_t)pid, good, crash_on && cw != 0u, dm, hf, cw);
     return assemble(pid, good, goodS, CB, CN, dm, hf);
   }
 };

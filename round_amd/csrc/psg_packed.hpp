@@ -169,7 +169,7 @@ PSG_DEV void pk_kagree_check_m(const Pk<W>& P, Checks& ck, int c, int kk, const 
 
 // Per-instance epilogue of a packed instance (finish_instance for W slots per lane):
 // the same digest (a sum over processes), decide results, summaries and counters.
-template <int W>
+template <int W, bool OPAQUE = true>
 PSG_DEV void pk_finish(const Pk<W>& P, const KArgs& a, uint64_t i, const Checks& ck, int nchecks,
                        const int32_t (&dec_val)[W], const int32_t (&dec_round)[W], const int32_t (&halt_round)[W],
                        const int32_t (&main_x)[W], BlockCounters* bc) {
@@ -182,7 +182,7 @@ PSG_DEV void pk_finish(const Pk<W>& P, const KArgs& a, uint64_t i, const Checks&
     if (!P.val[j]) continue;
     const int pid = P.pid(j);
     const bool decided = dec_round[j] >= 0;
-    d += proc_digest(pid, dec_val[j], dec_round[j], halt_round[j], main_x[j]);
+    d += proc_digest<OPAQUE>(pid, dec_val[j], dec_round[j], halt_round[j], main_x[j]);
     nd_l += decided ? 1u : 0u;
     const int32_t steps = halt_round[j] >= 0 ? halt_round[j] + 1 : a.R;
     steps_l += (uint32_t)steps;
