@@ -65,7 +65,7 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
     uint32_t u = (1u - dec01) | od | ne01(decision, p0) | irr01;
     if constexpr (!V2) u |= ox;  // keepInit (OTR only)
     if (!g.any((u & valid01) != 0u)) {
-      const int cnt = mpopc(g.ballot_any((valid01 & eq01(x, p0)) != 0u));
+      const int cnt = mpopc(g.ballot(x == p0));  // (a compare and the valid-lane mask)
       const uint32_t fb = (V2 ? 0u : fbit(cnt > sthr, 1)) | fbit(cnt == n, 2);
       ck.record(fb, true, c, g.lane);
       return;
