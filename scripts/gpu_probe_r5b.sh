@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 4: OTR settled-state witness test split into two wave-local ballots (W = 1) — parity, A/B.
+# Round 4: OTR micro-changes in the check — parity, A/B against the last commit.
 OUT=gpurun_out/r5b; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sampled.py -m gpu -q -x -k "otr or OTR" -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -3 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
 run() { PSG_LIB=round_amd/$1.so timeout -k 10 240 python3 scripts/probe_ab.py $2 > $OUT/$1_$2.log 2>&1 || exit $?; echo "== $1 $2"; cat $OUT/$1_$2.log; }
-for L in cnt libpsg cnt libpsg; do run $L otr; done
+for L in head libpsg head libpsg; do run $L otr; done
