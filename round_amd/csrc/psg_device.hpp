@@ -202,6 +202,9 @@ PSG_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 #ifndef PSG_AB_NO_CW
 #define PSG_AB_NO_CW 0  // A/B builds only: 1 = no survival-call skip
 #endif
+#ifndef PSG_PHILOX_OPAQUE_KEYS
+#define PSG_PHILOX_OPAQUE_KEYS 0
+#endif
 #ifndef PSG_PHILOX_MAD64
 #define PSG_PHILOX_MAD64 2  // 2: carry-out in VCC (no SGPR pair per product: fused OTR -1.8 %, gpu_probe_r4r.sh)
 #endif
@@ -221,6 +224,11 @@ PSG_DEV uint64_t mul64_mad(uint32_t a, uint32_t b) {
 #define PSG_MUL64(r, a, b) ((uint64_t)(a) * (b))
 #endif
 PSG_DEV U4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#if PSG_PHILOX_OPAQUE_KEYS && defined(__HIP_DEVICE_COMPILE__)
+  // the round keys are formed per call (18 scalar adds) instead of hoisted out of the kernel's
+  // loops into 20 SGPRs that then spill to VGPR lanes
+  asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = PSG_MUL64(r, 0xD2511F53u, c0);
@@ -1080,7 +1088,12 @@ struct Sched {
     uint32_t cw = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) cw |= CN.w[w] ? 1u << w : 0u;
+#ifdef PSG_ABL_NODRAW  // probe builds only: no words drawn (drop-free, crash-free schedules unaffected)
+#pragma unroll
+    for (int w = 0; w < W; ++w) dm[w] = hf[w] = ~0ull;
+#else
     draw<SKIP>((uint32_t)k, (uint32_t)pid, good, crash_on && cw != 0u, dm, hf, cw);
+#endif
     return assemble(pid, good, goodS, CB, CN, dm, hf);
   }
 };

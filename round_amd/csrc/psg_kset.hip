@@ -8,6 +8,11 @@
 // Payloads (decider, t) are staged in LDS; each process walks the alive senders
 // with broadcast LDS reads. `content.find(_._1)` (47-53) takes the LAST decider
 // message in Scala Map iteration order (CHAMP for > 4 entries).
+// Philox round keys formed per call in this translation unit (packed KSet C4 -3..5 %; the hoisted
+// 20-SGPR key schedule spilled here — and won in OTR / LastVoting / FloodMin / BenOr: r5d)
+#ifndef PSG_PHILOX_OPAQUE_KEYS
+#define PSG_PHILOX_OPAQUE_KEYS 1
+#endif
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
 #include "psg_packed.hpp"
@@ -338,7 +343,11 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
         uint32_t becomeDec = 0;
         const bool halted = halt_round[j] >= 0;  // before this round (set below when it decides)
         const uint32_t decider = (fw >> j) & 1u;
+#ifdef PSG_ABL_NOHO  // probe builds only (wrong results): every alive sender heard
+        const Mask<W> M = act;
+#else
         const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
+#endif
         const uint32_t live = P.val[j] & (halted ? 0u : 1u) & (1u - decider);
         const uint32_t hc = many(mand(M, Dm)) ? 1u : 0u;
         const uint32_t adopt = live & hc, mergep = live & (1u - hc);

@@ -9,6 +9,11 @@
 // value whose sender set meets its mailbox; with the self bit a receiver also
 // stops at its own estimate. Spec: TrivialSpec; the build checks k-agreement over
 // never-crashed deciders and validity, like KSetAgreement.
+// Philox round keys formed per call in this translation unit (packed KSetEarlyStopping -3.6 %; the hoisted
+// 20-SGPR key schedule spilled here — and won in OTR / LastVoting / FloodMin / BenOr: r5d)
+#ifndef PSG_PHILOX_OPAQUE_KEYS
+#define PSG_PHILOX_OPAQUE_KEYS 1
+#endif
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
 #include "psg_packed.hpp"
