@@ -1045,6 +1045,24 @@ struct Sched {
       hf[w] = ~0ull;
     }
     constexpr bool kSkip = SKIP && W > 1 && !PSG_AB_NO_CW;
+    if constexpr (kSkip) {
+      // loss-free schedules (C4) in crash rounds: only the survival words, W / 2 unrolled calls
+      // instead of the runtime-bounded word loop (packed KSet f = 64 7.63 -> 6.32 ms, KSetES -5.5 %,
+      // f = 1 +3.5 %: scripts/probes/gpu_probe_r5f.sh)
+      if (drop == 0 && crash) {
+        {
+#pragma unroll
+          for (int sc2 = 0; 2 * sc2 < W; ++sc2) {
+            if (!((cw >> (2 * sc2)) & 3u)) continue;  // neither word's 64 pids crash in round k
+            const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), k, pid + ((uint32_t)sc2 << 16),
+                                  (uint32_t)seed, (uint32_t)(seed >> 32));
+            hf[2 * sc2] = (uint64_t)o.x | ((uint64_t)o.y << 32);
+            if (2 * sc2 + 1 < W) hf[2 * sc2 + 1] = (uint64_t)o.z | ((uint64_t)o.w << 32);
+          }
+        }
+        return;
+      }
+    }
     draw_words<kSkip>(k, pid, j0, j1, nd, cw, dm, hf);
 #ifdef PSG_ABL_CHEAP_SURV  // probe builds only (wrong results): survival words without Philox
     if (crash) {
