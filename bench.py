@@ -38,6 +38,7 @@ from round_amd import psync  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 CUS = 256  # MI355X compute units (8 XCDs x 32)
+SPEC_CLOCK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md)
 
 
 def parse(argv=None):
@@ -373,6 +374,9 @@ def main(argv=None):
                 "process_rounds_active": s.active_process_rounds,
                 "instance_rounds_live": s.live_instance_rounds,
                 "instance_rounds_check_only": s.instances * args.rounds - s.live_instance_rounds,
+                # the same wall time over the process-rounds in which a process took a step
+                "active_rate": s.active_process_rounds * steps / head["dt"],
+                "active_rate_unit": "active process-rounds/s",
             },
             "variants": variants,
         }
@@ -383,9 +387,10 @@ def main(argv=None):
             # live rate of this run: the profile's instructions per instance-round (a property of
             # the code, valid only for the libpsg.so it was taken on) x the launch's
             # instance-rounds / this run's kernel time; peak: one instruction per CU per cycle
-            # (SALU) / per SIMD per 2 cycles (VALU, wave64 on a 32-lane SIMD) at the profile's clock
+            # (SALU) / per SIMD per 2 cycles (VALU, wave64 on a 32-lane SIMD) at the 2.4 GHz
+            # spec clock (the profile's measured clock is reported beside it, labelled)
             ipr = d["per_instance_round"]
-            clk = d.get("clock_GHz") or 2.4
+            clk = SPEC_CLOCK_GHZ
             salu = ipr["SQ_INSTS_SALU"] * inst_rounds / head["kernel_s"] / 1e9
             valu = ipr["SQ_INSTS_VALU"] * inst_rounds / head["kernel_s"] / 1e9
             pk_s, pk_v = CUS * clk, CUS * 4 * clk / 2
@@ -397,6 +402,11 @@ def main(argv=None):
                 rl.update({"pipe": pipe, "achieved": salu if pipe == "SALU" else valu,
                            "peak": pk_s if pipe == "SALU" else pk_v, "unit": f"G {pipe} instructions/s"})
                 rl["frac"] = rl["achieved"] / rl["peak"]
+                mclk = d.get("clock_GHz")
+                if mclk:
+                    rl["measured_clock"] = {"clock_GHz": mclk, "peak": rl["peak"] * mclk / clk,
+                                            "frac": rl["achieved"] / (rl["peak"] * mclk / clk),
+                                            "note": "the same rate against the profile's measured clock"}
                 rl["valu"] = {"achieved": valu, "peak": pk_v, "frac": valu / pk_v, "unit": "G VALU instructions/s"}
                 rl["salu"] = {"achieved": salu, "peak": pk_s, "frac": salu / pk_s, "unit": "G SALU instructions/s"}
                 rl["insts_per_instance_round"] = ipr

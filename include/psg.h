@@ -334,14 +334,20 @@ int psg_spec_compile_native(const char* text, int32_t alg, int32_t fused, int32_
  * (hoisted conjuncts free of a bound variable, split foralls), as Formula text — invariants
  * already guarded by their round invariants, (phase 1) — so the rewrites can be checked
  * against the Spec as written under any evaluator (tests). Same buffer contract as
- * psg_spec_native_source. PSG_SPEC_OPTIONS (environment, comma-separated) holds generator
- * options for all three entry points: nosym, nosplit, D<NAME>=<VALUE>. */
+ * psg_spec_native_source. Generator options for all three entry points (comma-separated:
+ * nosym, nosplit, D<NAME>=<VALUE>) come from psg_spec_set_options on the calling thread, else
+ * from the environment variable PSG_SPEC_OPTIONS; an unknown option, or a define naming a
+ * probe-build switch (PSG_AB*), makes the entry point return PSG_EINVAL. */
 int psg_spec_rewrite_text(const char* text, int32_t alg, char* out, size_t* out_len, char* err, size_t err_len);
 /* The HIP source psg_spec_compile_native compiles for these arguments (tests, inspection):
  * *src_len = capacity in, the size needed (with the terminating NUL) out; PSG_ERANGE when
  * src is NULL or too small. */
 int psg_spec_native_source(const char* text, int32_t alg, int32_t fused, int32_t n, char* src, size_t* src_len,
                            char* err, size_t err_len);
+/* The generator options of the CALLING THREAD for the three entry points above (thread-local:
+ * concurrent callers with different options never see each other's); NULL = back to the
+ * environment's PSG_SPEC_OPTIONS. PSG_EINVAL (and nothing changed) for an invalid string. */
+int psg_spec_set_options(const char* options);
 
 /* Real-valued algorithms (PSG_ALG_EPSILON, RealConsensusIO, Epsilon.scala:10-13).
  * Same contracts as the int32 entry points; other algorithms get PSG_EINVAL.

@@ -279,7 +279,8 @@ __global__ void bitset_selftest_kernel(const int32_t* ops, int n_ops, int32_t* o
   Mask<W> m = mzero<W>();
   int o = 0;
   for (int i = 0; i < n_ops; ++i) {
-    const int op = ops[2 * i], pos = (int)((uint32_t)ops[2 * i + 1] % (uint32_t)(64 * W));  // index mod 64 (mod 64W)
+    // index mod 64W on the signed value (Java's shift masks to mod 64 for W = 1; -1 -> 64W - 1)
+    const int op = ops[2 * i], pos = ((ops[2 * i + 1] % (64 * W)) + 64 * W) % (64 * W);
     switch (op) {
       case 0: m = mzero<W>(); break;
       case 1: m = mfull<W>(64 * W); break;

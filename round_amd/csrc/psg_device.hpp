@@ -154,7 +154,11 @@ struct PhaseTimers {
 #endif
   }
   // event-count builds (-DPSG_PHASE_TIMERS=2): mark() is off, the slots count events instead
-  PSG_DEV void add(int j, uint64_t v) { acc[j] += v; }
+  PSG_DEV void add(int j, uint64_t v) {
+#if PSG_PHASE_TIMERS == 2
+    acc[j] += v;
+#endif
+  }
   PSG_DEV void flush(unsigned long long* g, int lane) {
     const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
@@ -197,16 +201,13 @@ PSG_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // Philox's 32x32 -> 64-bit products as one v_mad_u64_u32 each (the compiler's v_mul_lo_u32 +
-// v_mul_hi_u32 pair measured 7 % slower per call, scripts/mb_philox.hip; the headline -1.4 %).
+// v_mul_hi_u32 pair measured 7 % slower per call, round-4 microbenchmark; the headline -1.4 %).
 // Round 0's products stay in C: their operands are often wave-uniform (scalar multiplies).
-#ifndef PSG_AB_NO_CW
-#define PSG_AB_NO_CW 0  // A/B builds only: 1 = no survival-call skip
-#endif
 #ifndef PSG_PHILOX_OPAQUE_KEYS
 #define PSG_PHILOX_OPAQUE_KEYS 0
 #endif
 #ifndef PSG_PHILOX_MAD64
-#define PSG_PHILOX_MAD64 2  // 2: carry-out in VCC (no SGPR pair per product: fused OTR -1.8 %, gpu_probe_r4r.sh)
+#define PSG_PHILOX_MAD64 2  // 2: carry-out in VCC (no SGPR pair per product: fused OTR -1.8 %, round-4 A/B)
 #endif
 #if PSG_PHILOX_MAD64 && defined(__HIP_DEVICE_COMPILE__)
 PSG_DEV uint64_t mul64_mad(uint32_t a, uint32_t b) {
@@ -323,7 +324,7 @@ PSG_DEV uint64_t proc_digest(int pid, int32_t dec, int32_t dround, int32_t hroun
 #if defined(__HIP_DEVICE_COMPILE__)
   // opaque copy: the pid term is recomputed per instance instead of hoisted out of the instance
   // loop and kept live (spilled to scratch) across every round (packed KSet's 12 B of scratch,
-  // FloodMin -2..5 %); packed BenOr keeps the hoisted form (3.6 % faster, gpu_probe_r4v.sh)
+  // FloodMin -2..5 %); packed BenOr keeps the hoisted form (3.6 % faster, round-4 A/B)
   if constexpr (OPAQUE) asm volatile("" : "+v"(pid));
 #endif
   uint64_t y = ((uint64_t)(uint32_t)pid << 32) | ((uint64_t)((uint32_t)dround & 0xFFFFu) << 16) |
@@ -1028,28 +1029,24 @@ struct Sched {
   }
   // SKIP = false: the plain loop (BenOr: the skip test in every call measured 9 % slower on its
   // crash-free C5 rows, a skip-only-in-crash-rounds second loop 2.5 % slower on packed KSet;
-  // scripts/gpu_probe_r4v.sh, r4w)
+  // round-4 A/Bs)
   template <bool SKIP = true>
   PSG_DEV void draw(uint32_t k, uint32_t pid, bool good, bool crash, uint64_t (&dm)[W], uint64_t (&hf)[W],
                     uint32_t cw = ~0u) const {
     const uint32_t nd = (uint32_t)W * drop;
     const uint32_t j0 = good ? nd : 0u;
-#ifdef PSG_ABL_CHEAP_SURV
-    const uint32_t j1 = good ? 0u : nd;
-#else
     const uint32_t j1 = crash ? nd + (uint32_t)W : (good ? 0u : nd);
-#endif
 #pragma unroll
     for (int w = 0; w < W; ++w) {
       dm[w] = ~0ull;
       hf[w] = ~0ull;
     }
-    constexpr bool kSkip = SKIP && W > 1 && !PSG_AB_NO_CW;
+    constexpr bool kSkip = SKIP && W > 1;
     if constexpr (kSkip) {
       // loss-free schedules (C4) in crash rounds: only the survival words, W / 2 unrolled calls
       // instead of the runtime-bounded word loop (packed KSet f = 64 7.63 -> 6.32 ms, KSetES -5.5 %,
-      // f = 1 +3.5 %: scripts/probes/gpu_probe_r5f.sh)
-      if (__builtin_expect(drop == 0 && crash, 0)) {  // (laid out of line: packed KSet -1.5 %, r5g)
+      // f = 1 +3.5 %: round-4 A/B)
+      if (__builtin_expect(drop == 0 && crash, 0)) {  // (laid out of line: packed KSet -1.5 %)
         {
 #pragma unroll
           for (int sc2 = 0; 2 * sc2 < W; ++sc2) {
@@ -1064,15 +1061,6 @@ struct Sched {
       }
     }
     draw_words<kSkip>(k, pid, j0, j1, nd, cw, dm, hf);
-#ifdef PSG_ABL_CHEAP_SURV  // probe builds only (wrong results): survival words without Philox
-    if (crash) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const uint64_t x = (inst ^ ((uint64_t)k << 40) ^ ((uint64_t)pid << 20) ^ (uint64_t)w) * 0x9E3779B97F4A7C15ull;
-        hf[w] = x ^ (x >> 29);
-      }
-    }
-#endif
   }
 
   // HO(pid) from its raw words. CB = processes crashed before round k, CN =
@@ -1106,12 +1094,7 @@ struct Sched {
     uint32_t cw = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) cw |= CN.w[w] ? 1u << w : 0u;
-#ifdef PSG_ABL_NODRAW  // probe builds only: no words drawn (drop-free, crash-free schedules unaffected)
-#pragma unroll
-    for (int w = 0; w < W; ++w) dm[w] = hf[w] = ~0ull;
-#else
     draw<SKIP>((uint32_t)k, (uint32_t)pid, good, crash_on && cw != 0u, dm, hf, cw);
-#endif
     return assemble(pid, good, goodS, CB, CN, dm, hf);
   }
 };

@@ -9,7 +9,7 @@
 // with broadcast LDS reads. `content.find(_._1)` (47-53) takes the LAST decider
 // message in Scala Map iteration order (CHAMP for > 4 entries).
 // Philox round keys formed per call in this translation unit (packed KSet C4 -3..5 %; the hoisted
-// 20-SGPR key schedule spilled here — and won in OTR / LastVoting / FloodMin / BenOr: r5d)
+// 20-SGPR key schedule spilled here — and won in OTR / LastVoting / FloodMin / BenOr: round-4 A/B)
 #ifndef PSG_PHILOX_OPAQUE_KEYS
 #define PSG_PHILOX_OPAQUE_KEYS 1
 #endif
@@ -197,9 +197,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
       decided[j] = halt_round[j] >= 0 ? 1u : 0u;
       notinit[j] = (fw >> (8 + j)) & 1u;
     }
-#ifndef PSG_ABL_NOCHECK  // probe builds only (wrong results): check points skipped
     pk_kagree_check_m<W>(P, ck, c, kk, decided, decision, cr, notinit);
-#endif
   };
   check(0);
   pt.mark(0);
@@ -343,11 +341,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
         uint32_t becomeDec = 0;
         const bool halted = halt_round[j] >= 0;  // before this round (set below when it decides)
         const uint32_t decider = (fw >> j) & 1u;
-#ifdef PSG_ABL_NOHO  // probe builds only (wrong results): every alive sender heard
-        const Mask<W> M = act;
-#else
         const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
-#endif
         const uint32_t live = P.val[j] & (halted ? 0u : 1u) & (1u - decider);
         const uint32_t hc = many(mand(M, Dm)) ? 1u : 0u;
         const uint32_t adopt = live & hc, mergep = live & (1u - hc);

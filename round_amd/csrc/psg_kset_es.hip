@@ -10,7 +10,7 @@
 // stops at its own estimate. Spec: TrivialSpec; the build checks k-agreement over
 // never-crashed deciders and validity, like KSetAgreement.
 // Philox round keys formed per call in this translation unit (packed KSetEarlyStopping -3.6 %; the hoisted
-// 20-SGPR key schedule spilled here — and won in OTR / LastVoting / FloodMin / BenOr: r5d)
+// 20-SGPR key schedule spilled here — and won in OTR / LastVoting / FloodMin / BenOr: round-4 A/B)
 #ifndef PSG_PHILOX_OPAQUE_KEYS
 #define PSG_PHILOX_OPAQUE_KEYS 1
 #endif

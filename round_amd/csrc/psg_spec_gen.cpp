@@ -35,29 +35,50 @@ namespace {
 // ------------------------------------------------------------------ tree helpers
 bool is_var(const Tree& T, int e, int uid) { return T.nodes[e].k == VAR && T.nodes[e].uid == uid; }
 
-// Generator options (experiments and profiling builds), from the environment variable
-// PSG_SPEC_OPTIONS, comma-separated: "nosym" (no symmetric-check-point lowering), "nosplit"
-// (no split foralls / hoisted conjuncts), "D<NAME>=<VALUE>" (a #define at the top of the
-// module, e.g. DPSG_PHASE_TIMERS=1). They change the source, hence the cache key.
+// Generator options (experiments and profiling builds), comma-separated: "nosym" (no
+// symmetric-check-point lowering), "nosplit" (no split foralls / hoisted conjuncts),
+// "D<NAME>=<VALUE>" (a #define at the top of the module, e.g. DPSG_PHASE_TIMERS=1). They change
+// the source, hence the cache key. Per thread: psg_spec_set_options sets the calling thread's
+// string, otherwise the environment variable PSG_SPEC_OPTIONS is read; every entry point parses
+// them into its own thread's GenOptions, so concurrent callers (JVM threads) never share state.
 struct GenOptions {
   bool symmetric = true, split = true;
   std::vector<std::string> defines;
 };
-GenOptions g_opts;  // set by load_options() before each generation (the entry points)
-void load_options() {
-  g_opts = GenOptions{};
-  const char* e = std::getenv("PSG_SPEC_OPTIONS");
-  std::string t = e ? e : "";
+thread_local GenOptions g_opts;        // this thread's options for the generation in progress
+thread_local std::string t_options;     // psg_spec_set_options (this thread)
+thread_local bool t_options_set = false;
+
+GenOptions parse_options(const std::string& t) {
+  GenOptions o;
   size_t i = 0;
   while (i <= t.size()) {
     const size_t j = t.find(',', i);
     const std::string tok = t.substr(i, j == std::string::npos ? std::string::npos : j - i);
-    if (tok == "nosym") g_opts.symmetric = false;
-    else if (tok == "nosplit") g_opts.split = false;
-    else if (tok.size() > 1 && tok[0] == 'D') g_opts.defines.push_back(tok.substr(1));
-    else if (!tok.empty()) throw SpecError("PSG_SPEC_OPTIONS: unknown option " + tok);
+    if (tok == "nosym") o.symmetric = false;
+    else if (tok == "nosplit") o.split = false;
+    else if (tok.size() > 1 && tok[0] == 'D') {
+      const std::string name = tok.substr(1, tok.find('=') == std::string::npos ? std::string::npos : tok.find('=') - 1);
+      if (name.empty() || name.find_first_not_of("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789_") !=
+                              std::string::npos)
+        throw SpecError("PSG_SPEC_OPTIONS: bad define " + tok);
+#ifndef PSG_PROBE_BUILD
+      // ablation / A-B switches of probe builds change results: never in a product module
+      if (name.compare(0, 6, "PSG_AB") == 0) throw SpecError("PSG_SPEC_OPTIONS: " + name + " needs a probe build");
+#endif
+      o.defines.push_back(tok.substr(1));
+    } else if (!tok.empty()) throw SpecError("PSG_SPEC_OPTIONS: unknown option " + tok);
     if (j == std::string::npos) break;
     i = j + 1;
+  }
+  return o;
+}
+void load_options() {
+  if (t_options_set) {
+    g_opts = parse_options(t_options);
+  } else {
+    const char* e = std::getenv("PSG_SPEC_OPTIONS");
+    g_opts = parse_options(e ? e : "");
   }
 }
 
@@ -1224,7 +1245,7 @@ std::string module_source(ParsedSpec& P, const Compiled& prog, int alg, bool fus
     if (n > 0) waves.push_back((n + 63) / 64);
     else waves = {1, 2, 3, 4};
     // the compiler's mul_lo / mul_hi Philox products: the inline v_mad_u64_u32 form that wins in the
-    // library's round kernels measured 4-6 % slower in the fused modules (scripts/gpu_probe_r4r.sh)
+    // library's round kernels measured 4-6 % slower in the fused modules (round-4 A/B)
     src = "#define PSG_FUSED_MODULE 1\n#ifndef PSG_PHILOX_MAD64\n#define PSG_PHILOX_MAD64 0\n#endif\n" + src + fused_source(alg, waves);
   }
   return src;
@@ -1360,6 +1381,23 @@ int compile_module(const std::string& src, int alg, bool fused, const char* cach
 }  // namespace psgspec
 
 extern "C" {
+
+int psg_spec_set_options(const char* options) {
+  using namespace psgspec;
+  if (!options) {
+    t_options_set = false;
+    t_options.clear();
+    return PSG_OK;
+  }
+  try {
+    (void)parse_options(options);
+  } catch (const std::exception&) {
+    return PSG_EINVAL;
+  }
+  t_options = options;
+  t_options_set = true;
+  return PSG_OK;
+}
 
 int psg_spec_native_source(const char* text, int32_t alg, int32_t fused, int32_t n, char* src, size_t* src_len,
                            char* err, size_t err_len) {

@@ -26,6 +26,7 @@ EXPORTED_SYMBOLS = [
     "psg_run_batch_spec", "psg_load_schedule", "psg_clear_schedule", "psg_materialize_schedule",
     "psg_population_fresh", "psg_population_next", "psg_population_read", "psg_spec_from_text", "psg_spec_release",
     "psg_spec_compile_native", "psg_spec_native_source", "psg_selftest_bitset", "psg_spec_rewrite_text",
+    "psg_spec_set_options",
 ]
 
 
@@ -89,6 +90,7 @@ def load():
                                             C.c_size_t]
         L.psg_selftest_bitset.argtypes = [C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.c_int32,
                                           C.POINTER(C.c_int32), C.c_int32]
+        L.psg_spec_set_options.argtypes = [C.c_char_p]
     except AttributeError:
         pass
     L.psg_spec_release.argtypes = [C.POINTER(abi.SpecProgram)]
@@ -379,23 +381,19 @@ def spec_from_text(text, alg=0):
 
 
 class _SpecOptions:
-    """PSG_SPEC_OPTIONS (the generator's options, psg.h) for the duration of one call."""
+    """The generator's options (psg.h psg_spec_set_options) on the calling thread for the
+    duration of one call; the environment is not touched, so threads never share them."""
 
     def __init__(self, options):
         self.options = ",".join(options)
 
     def __enter__(self):
-        self.saved = os.environ.get("PSG_SPEC_OPTIONS")
-        if self.options:
-            os.environ["PSG_SPEC_OPTIONS"] = self.options
-        else:
-            os.environ.pop("PSG_SPEC_OPTIONS", None)
+        from . import formula
+        if load().psg_spec_set_options(self.options.encode()) != 0:
+            raise formula.FormulaError(f"invalid generator options {self.options!r}")
 
     def __exit__(self, *exc):
-        if self.saved is None:
-            os.environ.pop("PSG_SPEC_OPTIONS", None)
-        else:
-            os.environ["PSG_SPEC_OPTIONS"] = self.saved
+        load().psg_spec_set_options(None)
 
 
 def spec_compile_native(text, alg=0, fused=False, n=0, cache_dir=None, options=()):

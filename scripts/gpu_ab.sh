@@ -1,14 +1,13 @@
 #!/bin/bash
-# A/B of two library builds on config rows (same box, same call).
-# usage: bash scripts/gpu_ab.sh TAG "prefixes" libA libB ...
-TAG=$1; ONLY=$2; shift 2
-mkdir -p gpurun_out/$TAG
-for L in "$@"; do
-  echo "== $L"
-  PSG_LIB=round_amd/$L.so timeout -k 10 200 python3 bench_configs.py --only "$ONLY" --steps 2 --warmup 1 > gpurun_out/$TAG/$L.log 2>&1 || exit 1
-  grep "^{" gpurun_out/$TAG/$L.log | python3 -c '
-import json, sys
-for l in sys.stdin:
-    d = json.loads(l); print(d["config"], round(d["kernel_ms"], 2), "%.3g" % d["value"])
-'
+# A/B of library builds (scripts/build_variant.sh NAME ...) on one box in one call:
+# scripts/probe_ab.py WHICH (otr | lv | kset | fm | kses | benor | slv | eps) per build, min kernel
+# ms over 5 launches. A failing step ends the script (no further GPU work).
+# usage: bash scripts/gpu_ab.sh TAG WHICH[,WHICH...] libA libB ...   (libpsg = the in-tree build)
+TAG=$1; WHICH=$2; shift 2
+OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
+for w in ${WHICH//,/ }; do
+  for L in "$@"; do
+    PSG_LIB=round_amd/$L.so timeout -k 10 240 python3 scripts/probe_ab.py $w > $OUT/${L}_$w.log 2>&1 || exit $?
+    echo "== $L $w"; cat $OUT/${L}_$w.log
+  done
 done

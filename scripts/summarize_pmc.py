@@ -131,8 +131,8 @@ for k in kernels:
                     "traffic_GBps": (fetch + write) / ns}
         if bpr:
             alg = inst * R * n * bpr
-            o["hbm"].update({"algorithmic_bytes": alg, "algorithmic_GBps": alg / ns,
-                             "traffic_over_algorithmic": (fetch + write) / alg})
+            # SURVEY §8d's streamed-state bytes: bookkeeping (state stays on chip), never a rate
+            o["hbm"].update({"algorithmic_bytes": alg, "traffic_over_algorithmic": (fetch + write) / alg})
     out[name] = o
 
 json.dump(out, open(os.path.join(args.dst, "pmc_summary.json"), "w"), indent=1)

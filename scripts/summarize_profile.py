@@ -64,8 +64,7 @@ if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         "write_bytes": write,
         "traffic_bytes": fetch + write,
         "traffic_GBps": (fetch + write) / dur / 1e9,
-        "algorithmic_bytes": alg_bytes,
-        "algorithmic_GBps": alg_bytes / dur / 1e9,
+        "algorithmic_bytes": alg_bytes,  # SURVEY §8d streamed-state bookkeeping, not a bandwidth
         "traffic_over_algorithmic": (fetch + write) / alg_bytes,
         "note": "FETCH_SIZE doubled (gfx950 half-count of wide coalesced reads); reads here are 4 B/lane "
                 "(uncalibrated width), so the read side is bounded by [FETCH_SIZE, 2*FETCH_SIZE]",

@@ -38,6 +38,15 @@ def ensuring(mailbox_vals, v1):
     return all(cnt(v1) > cnt(v2) or v1 <= v2 for v2 in mailbox_vals)
 
 
+@pytest.fixture
+def mmor_check(oracle_mod):
+    """The oracle's ensuring check is off by default (the CPU baseline times the round alone)."""
+    L = oracle_mod.lib()
+    L.oracle_set_mmor_check(1)
+    yield
+    L.oracle_set_mmor_check(0)
+
+
 def _stats(oracle_mod, reset=False):
     import ctypes as C
     L = oracle_mod.lib()
@@ -47,7 +56,7 @@ def _stats(oracle_mod, reset=False):
 
 
 @pytest.mark.parametrize("alg", [psync.OTR(), psync.OTR2()], ids=["otr", "otr2"])
-def test_oracle_mmor_satisfies_otr2_ensuring(oracle_mod, alg):
+def test_oracle_mmor_satisfies_otr2_ensuring(oracle_mod, mmor_check, alg):
     _stats(oracle_mod, reset=True)
     for n, V, seed in ((4, 3, 1), (16, 4, 2), (64, 64, 3), (64, 2, 4)):
         cfg = psync.make_config(alg, n, 10, seed=seed, value_range=V)
@@ -56,7 +65,7 @@ def test_oracle_mmor_satisfies_otr2_ensuring(oracle_mod, alg):
     assert calls > 10000 and fails == 0, (calls, fails)
 
 
-def test_ensuring_catches_a_mutant_mmor(oracle_mod):
+def test_ensuring_catches_a_mutant_mmor(oracle_mod, mmor_check):
     """Variant 2 (an oracle-only mutant: mmor ties go to the LARGER value) violates it."""
     _stats(oracle_mod, reset=True)
     cfg = psync.make_config(psync.OTR2(variant=2), 16, 10, seed=5, value_range=4)
@@ -64,6 +73,13 @@ def test_ensuring_catches_a_mutant_mmor(oracle_mod):
     calls, fails = _stats(oracle_mod, reset=True)
     assert calls > 0 and fails > 0
     assert not ensuring([1, 1, 2, 2], 2) and ensuring([1, 1, 2, 2], 1) and ensuring([3, 3, 3, 1], 3)
+
+
+def test_ensuring_check_is_off_by_default(oracle_mod):
+    """Without the pin tests' switch the oracle runs mmor alone (what cpu_baseline times)."""
+    _stats(oracle_mod, reset=True)
+    oracle_mod.run(psync.make_config(psync.OTR(), 16, 10, seed=2, value_range=4), 0, 50, threads=2)
+    assert _stats(oracle_mod, reset=True) == (0, 0)
 
 
 @pytest.mark.gpu
@@ -426,3 +442,7 @@ def test_gpu_mask_passes_long_bitset_tests(W):
     # flip (LongBitSet.scala:9): involution, and equal to set / clear on the bit
     assert lib.selftest_bitset([("empty", 0), ("flip", 5), ("get", 5), ("flip", 5), ("get", 5), ("size", 0)], W) \
         == [1, 0, 0]
+    # negative positions wrap modulo 64W on the signed value (Java's `1L << -1` is bit 63 for W = 1)
+    size = 64 * W
+    assert lib.selftest_bitset([("empty", 0), ("set", -1), ("get", size - 1), ("set", -size - 2),
+                                ("get", size - 2), ("size", 0)], W) == [1, 1, 2]

@@ -43,7 +43,7 @@ def test_native_source_generates(cid, alg, n, text):
 
 
 def test_generator_options():
-    """PSG_SPEC_OPTIONS (psg.h): nosym drops the symmetric-check-point lowering, nosplit the
+    """Generator options (psg.h psg_spec_set_options / PSG_SPEC_OPTIONS): nosym drops the symmetric-check-point lowering, nosplit the
     split foralls, D<NAME>=<VALUE> adds a #define; the default source has neither change."""
     t = F.to_text(F.otr_spec())
     base = lib.spec_native_source(t, abi.PSG_ALG_OTR)
@@ -54,9 +54,69 @@ def test_generator_options():
     lv = F.to_text(F.lv_spec())
     assert lib.spec_native_source(lv, abi.PSG_ALG_LAST_VOTING) != lib.spec_native_source(
         lv, abi.PSG_ALG_LAST_VOTING, options=["nosplit"])
-    with pytest.raises(F.FormulaError, match="unknown option"):
+    with pytest.raises(F.FormulaError, match="invalid generator options"):
         lib.spec_native_source(t, abi.PSG_ALG_OTR, options=["bogus"])
     assert "PSG_SPEC_OPTIONS" not in os.environ
+
+
+def test_generator_options_are_per_thread():
+    """8 threads lower concurrently, each with its own options (psg_spec_set_options is
+    thread-local): every result equals the single-threaded result for those options."""
+    import threading
+    t_otr, t_lv = F.to_text(F.otr_spec()), F.to_text(F.lv_spec())
+    jobs = [(lib.spec_native_source, t_otr, abi.PSG_ALG_OTR, ()),
+            (lib.spec_native_source, t_otr, abi.PSG_ALG_OTR, ("nosym",)),
+            (lib.spec_native_source, t_lv, abi.PSG_ALG_LAST_VOTING, ("nosplit",)),
+            (lib.spec_native_source, t_otr, abi.PSG_ALG_OTR, ("DPSG_PHASE_TIMERS=1",)),
+            (lib.spec_rewrite_text, t_lv, abi.PSG_ALG_LAST_VOTING, ()),
+            (lib.spec_rewrite_text, t_lv, abi.PSG_ALG_LAST_VOTING, ("nosplit",)),
+            (lib.spec_native_source, t_lv, abi.PSG_ALG_LAST_VOTING, ("nosym", "DPSG_X=3")),
+            (lib.spec_rewrite_text, t_otr, abi.PSG_ALG_OTR, ("nosplit",))]
+    want = [fn(t, alg, options=o) for fn, t, alg, o in jobs]
+    got = [[] for _ in jobs]
+    errors = []
+
+    def worker(i):
+        fn, t, alg, o = jobs[i]
+        try:
+            for _ in range(12):
+                got[i].append(fn(t, alg, options=o))
+        except Exception as e:  # noqa: BLE001 — reported below
+            errors.append((i, e))
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(len(jobs))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    for i in range(len(jobs)):
+        assert all(g == want[i] for g in got[i]), i
+    # the options differ in effect, so a leak between threads would have shown
+    assert want[0] != want[1] and want[4] != want[5] and want[3].startswith("#define PSG_PHASE_TIMERS 1\n")
+
+
+def test_probe_switches_rejected():
+    """A define naming a probe-build switch (PSG_AB*) never reaches a product module: from the
+    per-thread setter and from the environment alike the entry points return PSG_EINVAL."""
+    import subprocess
+    import sys
+    t = F.to_text(F.otr_spec())
+    with pytest.raises(F.FormulaError, match="invalid generator options"):
+        lib.spec_native_source(t, abi.PSG_ALG_OTR, options=["DPSG_ABL_NOCHECK=1"])
+    L = lib.load()
+    assert L.psg_spec_set_options(b"DPSG_AB_NO_CW=1") == abi.PSG_EINVAL
+    assert L.psg_spec_set_options(b"D=1") == abi.PSG_EINVAL
+    # through the environment (the JVM route): a child process, rc of psg_spec_native_source
+    code = ("import ctypes as C, sys; sys.path.insert(0, %r); from round_amd import lib, formula as F, abi; "
+            "L = lib.load(); n = C.c_size_t(0); err = C.create_string_buffer(512); "
+            "rc = L.psg_spec_native_source(F.to_text(F.otr_spec()).encode(), abi.PSG_ALG_OTR, 0, 0, None, "
+            "C.byref(n), err, 512); print(rc, err.value.decode())") % os.path.dirname(os.path.dirname(
+                os.path.abspath(__file__)))
+    env = dict(os.environ, PSG_SPEC_OPTIONS="DPSG_ABL_NOCHECK=1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    rc, _, msg = out.stdout.strip().partition(" ")
+    assert int(rc) == abi.PSG_EINVAL and "probe build" in msg, out
 
 
 def test_native_source_rejects_like_the_bytecode_compiler():
