@@ -1307,8 +1307,8 @@ PSG_DEV bool tracing(const KArgs& a) {
 template <int W, class SH, class St>
 PSG_DEV void emit_state(St& sh, const Grp<W>& g, const KArgs& a, uint64_t i, int c, int32_t x, int32_t decided,
                         int32_t decision, int32_t ts, int32_t ready, int32_t commit, int32_t vote, int32_t cand,
-                        int32_t hosize) {
-  if constexpr (SH::kFused) sh.put(c, x, decided, decision, ts, ready, commit, vote, cand, hosize);
+                        int32_t hosize, bool frozen = false) {
+  if constexpr (SH::kFused) sh.put(c, x, decided, decision, ts, ready, commit, vote, cand, hosize, frozen);
   else trace_put<W>(g, a, i, c, x, decided, decision, ts, ready, commit, vote, cand, hosize);
 }
 

@@ -130,12 +130,43 @@ PSG_DEV int kset_find(const KArgs& a, const uint64_t* ts, const Mask<W>& M, cons
 template <int W>
 struct KsPk {
   static constexpr int kClasses = 8;
-  uint64_t ts[64 * W * W];
   int32_t x0s[64 * W];
   static constexpr int kCols = 32;
   uint64_t ct[kClasses][W];  // a round's classes of equal t among the alive senders: their t
   uint64_t ce[kClasses][W];  // ... and their members
   uint64_t hol[kCols][W];    // holders H_o of each varying origin o (column form, below)
+};
+
+// The pre-round t staging ([word][pid], 8 KB at W = 4) is needed only in the few rounds before
+// every alive t is equal (tuni) — two or three of an instance's rounds — so the block's four
+// waves share two buffers (wave w uses buffer w / 2) under an LDS lock instead of owning one
+// each: 52 -> 36 KB of LDS per block, four blocks per CU instead of three.
+#ifndef PSG_KSET_STAGE_BUFS
+#define PSG_KSET_STAGE_BUFS 2  // staging buffers per 4-wave block (wave w uses buffer w * BUFS / 4)
+#endif
+template <int W>
+struct KsStage {
+  static constexpr int kBufs = PSG_KSET_STAGE_BUFS;
+  uint64_t ts[kBufs][64 * W * W];
+  int lock[kBufs];
+  PSG_DEV void init() {
+    if (threadIdx.x < kBufs) lock[threadIdx.x] = 0;
+  }
+  // wave-uniform; no wave holding a buffer ever waits for another wave, so every waiter gets it
+  PSG_DEV uint64_t* acquire(int b, int lane) {
+    while (true) {
+      int got = 0;
+      if (lane == 0) got = atomicCAS(&lock[b], 0, 1) == 0 ? 1 : 0;
+      if (__builtin_amdgcn_readfirstlane(got)) break;
+      __builtin_amdgcn_s_sleep(4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return ts[b];
+  }
+  PSG_DEV void release(int b, int lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this wave's reads of ts done
+    if (lane == 0) atomicExch(&lock[b], 0);
+  }
 };
 
 // Wave AND / OR of a per-lane mask (DPP OR reductions; AND = NOT OR NOT).
@@ -150,8 +181,8 @@ PSG_DEV void pk_and_or(const Mask<W>& a, const Mask<W>& o, Mask<W>& all, Mask<W>
 }
 
 template <int W>
-PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, KsPk<W>& L, int32_t* x0lds,
-                         BlockCounters* bc, PhaseTimers& pt) {
+PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, KsPk<W>& L, KsStage<W>& S,
+                         int sbuf, int32_t* x0lds, BlockCounters* bc, PhaseTimers& pt) {
   const int n = a.n, kk = a.param;
   const int need = a.variant == 1 ? 1 : n - kk;  // same.size > n - k (KSetAgreement.scala:56)
   Sched<W, false> sc;
@@ -208,6 +239,11 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
     for (int j = 0; j < W; ++j) al[j] = P.val[j];
     act = P.ballot(al);
   }
+  // tuni: every alive process holds the same t. No round changes that (a merge's union and an
+  // adoption are that t again), so from the first round it holds on the staging, the round-0
+  // closed form and the classes / columns are skipped: same = |M|, t unchanged.
+  bool tuni = false;
+  const bool lazy = sc.drop == 0 && sc.ho_min < 0;  // crash-round survival words drawn on demand (below)
   for (int k = 0; k < a.R; ++k) {
     // Once every process halted the state is frozen; the round has no step to take, but its
     // check point is still evaluated (every counted process-round is checked).
@@ -227,20 +263,47 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
 #pragma unroll
       for (int j = 0; j < W; ++j) dw[j] = (fw >> j) & 1u;
       const Mask<W> Dm = mand(P.ballot(dw), act);  // senders' decider flags (pre-state)
-#pragma unroll
-      for (int j = 0; j < W; ++j)
-#pragma unroll
-        for (int w = 0; w < W; ++w) L.ts[w * 64 * W + P.pid(j)] = t[j].w[w];  // [word][pid]
-      lds_sync<1>();
       // round 0 (every alive sender still holds only its own origin): closed form below
-      uint32_t notown[W];
+      bool closed = false;
+      if (!tuni) {
+        uint32_t notown[W];
 #pragma unroll
-      for (int j = 0; j < W; ++j) {
-        Mask<W> own = mzero<W>();
-        if (P.val[j]) own.w[j] = 1ull << P.lane;
-        notown[j] = meq(t[j], own) ? 0u : 1u;
+        for (int j = 0; j < W; ++j) {
+          Mask<W> own = mzero<W>();
+          if (P.val[j]) own.w[j] = 1ull << P.lane;
+          notown[j] = meq(t[j], own) ? 0u : 1u;
+        }
+        closed = !many(mand(act, P.ballot(notown)));
       }
-      const bool closed = !many(mand(act, P.ballot(notown)));
+      // Every alive sender holding the same t (the common case once round 0 has spread the
+      // origins) is one compare per slot against the first alive sender's t (read from its
+      // lane) and a ballot; then tuni holds for the rest of the instance.
+      if (!tuni && !closed) {
+        const int q0 = mfirst(act), j0 = q0 >> 6, l0 = q0 & 63;
+        Mask<W> t0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          t0.w[w] = readlane64(t[0].w[w], l0);
+#pragma unroll
+          for (int j = 1; j < W; ++j)
+            if (j0 == j) t0.w[w] = readlane64(t[j].w[w], l0);
+        }
+        uint32_t dif = 0;
+#pragma unroll
+        for (int j = 0; j < W; ++j) dif |= (uint32_t)((act.w[j] >> P.lane) & 1ull) & (meq(t[j], t0) ? 0u : 1u);
+        tuni = !pk_any(dif);
+      }
+      // the pre-round t masks staged for the class reads and adoptions ([word][pid])
+      const bool staged = !tuni && (!closed || many(Dm));
+      uint64_t* ts = nullptr;
+      if (staged) {
+        ts = S.acquire(sbuf, P.lane);
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+#pragma unroll
+          for (int w = 0; w < W; ++w) ts[w * 64 * W + P.pid(j)] = t[j].w[w];
+        lds_sync<1>();
+      }
       // The classes of equal t among the alive senders (same = mailbox.filter(_._2._2 == t).size,
       // uni = t ++ every received t) are the same for every receiver: found once per round (at
       // most kClasses; the rest, rem, is walked sender by sender), their t and member masks kept
@@ -257,19 +320,8 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
       int ncls = 0, ncols = 0;
       uint32_t cls = 0xFFFFu;
       Mask<W> rem = act, D = mzero<W>();
-      bool cols = false;
-      // Every alive sender holding the same t (the common case once round 0 has spread the
-      // origins: D is empty) is one compare per slot against the first alive sender's t and
-      // a ballot, instead of the wave AND / OR reductions that find I and U (C4 f = 64 8.53 ->
-      // 8.0 ms, f = 1 2.17 -> 2.08 ms)
-      if (!closed) {
-        const Mask<W> t0 = load_t<W, 64 * W>(L.ts, mfirst(act));
-        uint32_t dif = 0;
-#pragma unroll
-        for (int j = 0; j < W; ++j) dif |= (uint32_t)((act.w[j] >> P.lane) & 1ull) & (meq(t[j], t0) ? 0u : 1u);
-        cols = !pk_any(dif);  // D is empty: the column form with no column
-      }
-      if (!closed && !cols) {
+      const bool cols = !tuni && !closed;
+      if (cols) {
         Mask<W> il, ul;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
@@ -289,9 +341,9 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
         pk_and_or<W>(il, ul, I, U);
         D = mandn(U, I);
         ncols = mpopc(D);
-        cols = ncols <= KsPk<W>::kCols;
       }
-      if (cols) {
+      const bool colform = cols && ncols <= KsPk<W>::kCols;
+      if (colform) {
         Mask<W> dd = D;
         for (int c = 0; c < ncols; ++c) {
           const int o = mtake_first(dd);
@@ -304,9 +356,9 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
             if (P.lane == w) L.hol[c][w] = H.w[w];
         }
         lds_sync<1>();
-      } else if (!closed) {
+      } else if (cols) {
         for (; ncls < KsPk<W>::kClasses && many(rem); ++ncls) {
-          const Mask<W> tq = load_t<W, 64 * W>(L.ts, mfirst(rem));
+          const Mask<W> tq = load_t<W, 64 * W>(ts, mfirst(rem));
           uint32_t mine[W];
 #pragma unroll
           for (int jj = 0; jj < W; ++jj) {
@@ -329,90 +381,141 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
       pt.mark(1);
       pt.add(0, 1);  // event-count builds: round paths (live, closed, uniform t, columns, classes)
       pt.add(1, closed);
-      pt.add(2, cols && ncols == 0);
-      pt.add(3, cols && ncols > 0);
-      pt.add(4, cols ? ncols : 0);
-      pt.add(5, !closed && !cols);
-      pt.add(6, !closed && !cols ? mpopc(rem) : 0);
+      pt.add(2, tuni);
+      pt.add(3, colform);
+      pt.add(4, colform ? ncols : 0);
+      pt.add(5, cols && !colform);
+      pt.add(6, cols && !colform ? mpopc(rem) : 0);
       pt.add(7, many(CN));
       // one slot at a time (its HO set M, its merge or adoption)
+      if (tuni) {
+        // Every sender's t is t_p, so a step reads its mailbox only through hc (some decider
+        // heard) and same = |M| > need (KSetAgreement.scala:46-58), and t never changes (a
+        // union or an adoption is t_p again). In a crash round (no benign loss, no ho_min) M
+        // lies between Mlo (every crashing sender's message lost) and Mhi (all delivered); when
+        // both bounds give the same hc and |M| > need for every live slot of the wave, the
+        // round's survival words change nothing and are not drawn (each is a pure function of
+        // (instance, round, pid): skipping one moves no other draw).
+        const bool lazyr = lazy && many(CN);
 #pragma unroll
-      for (int j = 0; j < W; ++j) {
-        uint32_t becomeDec = 0;
-        const bool halted = halt_round[j] >= 0;  // before this round (set below when it decides)
-        const uint32_t decider = (fw >> j) & 1u;
-        const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
-        const uint32_t live = P.val[j] & (halted ? 0u : 1u) & (1u - decider);
-        const uint32_t hc = many(mand(M, Dm)) ? 1u : 0u;
-        const uint32_t adopt = live & hc, mergep = live & (1u - hc);
-        Mask<W> tnew = t[j];
-        if (pk_any(mergep)) {
-          int same = 0;
-          Mask<W> uni = t[j];
-          if (closed) {
-            same = ((M.w[j] >> P.lane) & 1ull) ? 1 : 0;
-            uni = mor(t[j], M);
-          } else if (cols) {
-            Mask<W> Eq = act, dd = D;
-            for (int c = 0; c < ncols; ++c) {
-              const int o = mtake_first(dd);
-              Mask<W> H;
+        for (int j = 0; j < W; ++j) {
+          const bool halted = halt_round[j] >= 0;
+          const uint32_t decider = (fw >> j) & 1u;
+          const uint32_t live = P.val[j] & (halted ? 0u : 1u) & (1u - decider);
+          uint32_t hc, big;
+          bool exact = !lazyr;
+          if (lazyr) {
+            uint64_t one[W], zero[W];
 #pragma unroll
-              for (int w = 0; w < W; ++w) H.w[w] = L.hol[c][w];
-              const bool hit = many(mand(M, H));
-              const uint64_t bit = 1ull << (o & 63);
-              const bool mine = mtest(t[j], o);
+            for (int w = 0; w < W; ++w) {
+              one[w] = ~0ull;
+              zero[w] = 0ull;
+            }
+            const Mask<W> Mhi = mand(sc.assemble(P.pid(j), good, goodS, CB, CN, one, one), act);
+            const Mask<W> Mlo = mand(sc.assemble(P.pid(j), good, goodS, CB, CN, one, zero), act);
+            const uint32_t hlo = many(mand(Mlo, Dm)) ? 1u : 0u, hhi = many(mand(Mhi, Dm)) ? 1u : 0u;
+            const uint32_t plo = mpopc(Mlo) > need ? 1u : 0u, phi = mpopc(Mhi) > need ? 1u : 0u;
+            hc = hlo;
+            big = plo;
+            // undetermined: hc open, or no decider heard for sure and |M| > need open
+            exact = pk_any(live & ((hlo ^ hhi) | ((1u - hlo) & (plo ^ phi))));
+          }
+          if (exact) {
+            const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
+            hc = many(mand(M, Dm)) ? 1u : 0u;
+            big = mpopc(M) > need ? 1u : 0u;
+          }
+          pt.mark(6);  // (profiling builds: t6 = the slots' HO sets)
+          if (!halted && decider) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:48-50)
+            const int32_t v = kset_pick<W>(t[j], L.x0s, Emin, xmin);
+            decision[j] = v;
+            fw |= (1u - X0.contains01(v)) << (8 + j);
+            halt_round[j] = k;
+          }
+          fw |= (live & (hc | big)) << j;  // adopts, or merges with same > n - k: decider
+          pt.mark(2);
+        }
+      } else {
 #pragma unroll
-              for (int w = 0; w < W; ++w) {
-                uni.w[w] |= (hit && (o >> 6) == w) ? bit : 0ull;
-                Eq.w[w] &= mine ? H.w[w] : ~H.w[w];
+        for (int j = 0; j < W; ++j) {
+          uint32_t becomeDec = 0;
+          const bool halted = halt_round[j] >= 0;  // before this round (set below when it decides)
+          const uint32_t decider = (fw >> j) & 1u;
+          const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
+          pt.mark(6);
+          const uint32_t live = P.val[j] & (halted ? 0u : 1u) & (1u - decider);
+          const uint32_t hc = many(mand(M, Dm)) ? 1u : 0u;
+          const uint32_t adopt = live & hc, mergep = live & (1u - hc);
+          Mask<W> tnew = t[j];
+          if (pk_any(mergep)) {
+            int same = 0;
+            Mask<W> uni = t[j];
+            if (closed) {
+              same = ((M.w[j] >> P.lane) & 1ull) ? 1 : 0;
+              uni = mor(t[j], M);
+            } else if (colform) {
+              Mask<W> Eq = act, dd = D;
+              for (int c = 0; c < ncols; ++c) {
+                const int o = mtake_first(dd);
+                Mask<W> H;
+#pragma unroll
+                for (int w = 0; w < W; ++w) H.w[w] = L.hol[c][w];
+                const bool hit = many(mand(M, H));
+                const uint64_t bit = 1ull << (o & 63);
+                const bool mine = mtest(t[j], o);
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                  uni.w[w] |= (hit && (o >> 6) == w) ? bit : 0ull;
+                  Eq.w[w] &= mine ? H.w[w] : ~H.w[w];
+                }
+              }
+              same = mpopc(mand(M, Eq));
+            } else {
+              const int mc = (int)((cls >> (4 * j)) & 15u);
+              for (int c = 0; c < ncls; ++c) {
+                Mask<W> E, tq;
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                  E.w[w] = L.ce[c][w];
+                  tq.w[w] = L.ct[c][w];
+                }
+                const Mask<W> ME = mand(M, E);
+                if (c == mc) same = mpopc(ME);
+                if (many(ME)) uni = mor(uni, tq);
+              }
+              Mask<W> rr = rem;
+              while (many(rr)) {
+                const int q = mtake_first(rr);
+                const Mask<W> tq = load_t<W, 64 * W>(ts, q);
+                if (mtest(M, q)) {
+                  same += meq(tq, t[j]) ? 1 : 0;
+                  uni = mor(uni, tq);
+                }
               }
             }
-            same = mpopc(mand(M, Eq));
-          } else {
-            const int mc = (int)((cls >> (4 * j)) & 15u);
-            for (int c = 0; c < ncls; ++c) {
-              Mask<W> E, tq;
-#pragma unroll
-              for (int w = 0; w < W; ++w) {
-                E.w[w] = L.ce[c][w];
-                tq.w[w] = L.ct[c][w];
-              }
-              const Mask<W> ME = mand(M, E);
-              if (c == mc) same = mpopc(ME);
-              if (many(ME)) uni = mor(uni, tq);
-            }
-            Mask<W> rr = rem;
-            while (many(rr)) {
-              const int q = mtake_first(rr);
-              const Mask<W> tq = load_t<W, 64 * W>(L.ts, q);
-              if (mtest(M, q)) {
-                same += meq(tq, t[j]) ? 1 : 0;
-                uni = mor(uni, tq);
-              }
+            if (mergep) {
+              if (same > need) becomeDec = 1;
+              else tnew = uni;
             }
           }
-          if (mergep) {
-            if (same > need) becomeDec = 1;
-            else tnew = uni;
+          if (adopt) {  // t = content.find(_._1).get._2 — last decider message in iteration order
+            tnew = load_t<W, 64 * W>(ts, kset_find<W, 64 * W>(a, ts, M, mand(M, Dm), colform ? L.hol : nullptr, ncols));
+            becomeDec = 1;
           }
-        }
-        if (adopt) {  // t = content.find(_._1).get._2 — last decider message in iteration order
-          tnew = load_t<W, 64 * W>(L.ts, kset_find<W, 64 * W>(a, L.ts, M, mand(M, Dm), cols ? L.hol : nullptr, ncols));
-          becomeDec = 1;
-        }
-        if (!halted && decider) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:48-50)
-          const int32_t v = kset_pick<W>(t[j], L.x0s, Emin, xmin);
-          decision[j] = v;
-          fw |= (1u - X0.contains01(v)) << (8 + j);
-          halt_round[j] = k;
-        }
-        if (!halted) {  // the post-round state of slot j (its pre-round t is in the staging)
-          t[j] = tnew;
-          fw |= becomeDec << j;
+          if (!halted && decider) {  // decide(pick(t)); exitAtEndOfRound (KSetAgreement.scala:48-50)
+            const int32_t v = kset_pick<W>(t[j], L.x0s, Emin, xmin);
+            decision[j] = v;
+            fw |= (1u - X0.contains01(v)) << (8 + j);
+            halt_round[j] = k;
+          }
+          if (!halted) {  // the post-round state of slot j (its pre-round t is in the staging)
+            t[j] = tnew;
+            fw |= becomeDec << j;
+          }
+          pt.mark(2);
         }
       }
-      lds_sync<1>();  // all reads of ts done before the next round restages it
+      if (staged) S.release(sbuf, P.lane);  // all reads of ts (and hol / ct / ce) done
       uint32_t al[W];
 #pragma unroll
       for (int j = 0; j < W; ++j) {
@@ -428,7 +531,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
 #pragma unroll
   for (int j = 0; j < W; ++j) mainx[j] = P.val[j] ? kset_pick<W>(t[j], L.x0s, Emin, xmin) : 0;
   pk_finish<W>(P, a, i, ck, 2, decision, halt_round, halt_round, mainx, bc);
-  lds_sync<1>();  // x0s / ts reads done before the next instance restages them
+  lds_sync<1>();  // x0s reads done before the next instance restages them
   pt.mark(3);
 }
 
@@ -439,18 +542,20 @@ template <int W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_KSET_PK_WPE))) kset_packed_kernel(KArgs a) {
   __shared__ BlockCounters bc;
   __shared__ KsPk<W> L[4];
+  __shared__ KsStage<W> S;
   __shared__ int32_t x0tab[4][X0Set<W>::kSlots];
   counters_init(&bc);
+  S.init();
   __syncthreads();
   Pk<W> P;
   P.setup(a.n);
   const int grp = threadIdx.x >> 6;
   PhaseTimers pt;  // profiling builds only: t0 setup, t1 staging + classes, t2 slot updates, t3 finish,
-  pt.start();      // t4 check after a live round, t5 frozen round
+  pt.start();      // t4 check after a live round, t5 frozen round, t6 the slots' HO sets
   InstanceQueue<1> Q;
   for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
-    kset_packed<W>(P, a, i, inst, L[grp], x0tab[grp], &bc, pt);
+    kset_packed<W>(P, a, i, inst, L[grp], S, grp * KsStage<W>::kBufs / 4, x0tab[grp], &bc, pt);
   }
   pt.flush(a.counters, P.lane);
   __syncthreads();

@@ -167,8 +167,9 @@ PSG_DEV void otr_body(const KArgs& a) {
     typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
     if constexpr (!SH::kFused) otr_check<W, V2>(g, L, X0, ck, 0, false, n, full, x, dec01, decision, 0u, -1, valid01, od, ox);
     // OTR2's decision is an Option (PSG_NONE32 when empty)
-    auto trace = [&](int c, int32_t hs) {
-      emit_state<W, SH>(sh, g, a, i, c, x, (int32_t)dec01, V2 && !dec01 ? PSG_NONE32 : decision, 0, 0, 0, 0, 0, hs);
+    auto trace = [&](int c, int32_t hs, bool frozen = false) {
+      emit_state<W, SH>(sh, g, a, i, c, x, (int32_t)dec01, V2 && !dec01 ? PSG_NONE32 : decision, 0, 0, 0, 0, 0, hs,
+                        frozen);
     };
     if (tracing_on) trace(0, n);
     pt.mark(0);
@@ -274,7 +275,7 @@ PSG_DEV void otr_body(const KArgs& a) {
     for (int k = kf; k < a.R; ++k) {
       if constexpr (!SH::kFused)
         otr_check<W, V2, true>(g, L, X0, ck, k + 1, true, n, full, x, dec01, decision, dec01, decision, valid01, od, ox);
-      if (tracing_on) trace(k + 1, n);
+      if (tracing_on) trace(k + 1, n, true);
       pt.mark(2);
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 8, dec_val, dec_round, halt_round, x, &bc,

@@ -45,6 +45,10 @@ struct Ctx {
   // field the uniform lowering reads, process 0's in uc / uo; uni says whether it holds
   bool uni = false;
   int32_t uc[PSG_NFIELDS] = {0}, uo[PSG_NFIELDS] = {0};
+  // check points since the state last changed (fused hook, 0..2): at 2 the current and old fields
+  // are those of the previous check point, so what depends on the fields alone (the symmetric
+  // test, majority candidates, the staged copies) is still valid; the formulas are re-evaluated
+  int unch = 0;
   // member_init_u: per memo slot, the last probed (uniform) value and its membership
   uint32_t muok = 0;
   int32_t muv[4] = {0, 0, 0, 0}, mur[4] = {0, 0, 0, 0};
@@ -65,6 +69,7 @@ struct Ctx {
 // (LastVoting: crashed processes never decide) pays one broadcast and one ballot.
 template <int W, uint32_t CUR, uint32_t OLD>
 PSG_DEV bool uniform(Ctx<W>& x) {
+  if (x.unch >= 2) return x.uni;  // the same fields as at the previous check point
   constexpr int F0 = CUR ? __builtin_ctz(CUR) : -1;
   constexpr bool kTwo = F0 >= 0 && ((CUR & (CUR - 1)) | OLD) != 0u;  // more than one field
   if constexpr (kTwo) {
@@ -683,32 +688,38 @@ struct SpecHook {
     }
     PSG_DEV State(Grp<W>& g, int grp_, int n) : x{g, n, 0, {0}, {0}, {0}, stage_lds()}, grp(grp_) { ck.reset(); }
 
+    // frozen: no process took a step in the round before check point c (the kernel's frozen
+    // tail), so the state, old included, repeats; from the second such check point in a row the
+    // fields, their staged copies and what depends on them alone are kept (Ctx::unch)
     PSG_DEV void put(int c, int32_t f0, int32_t f1, int32_t f2, int32_t f3, int32_t f4, int32_t f5, int32_t f6,
-                     int32_t f7, int32_t f8) {
+                     int32_t f7, int32_t f8, bool frozen = false) {
       Grp<W>& g = x.g;
       const int32_t v[PSG_NFIELDS] = {f0, f1, f2, f3, f4, f5, f6, f7, f8};
       x.r = c;
-      x.maj_k0 = x.maj_k1 = -1;
+      x.unch = (frozen && c > 0) ? (x.unch < 2 ? x.unch + 1 : 2) : 0;
+      if (x.unch < 2) {
+        x.maj_k0 = x.maj_k1 = -1;
 #pragma unroll
-      for (int f = 0; f < PSG_NFIELDS; ++f) {
-        if (!((S::kFields >> f) & 1u)) continue;
-        const int32_t val = g.valid ? v[f] : 0;  // the trace holds valid processes only
+        for (int f = 0; f < PSG_NFIELDS; ++f) {
+          if (!((S::kFields >> f) & 1u)) continue;
+          const int32_t val = g.valid ? v[f] : 0;  // the trace holds valid processes only
+          if (c == 0) {
+            x.i[f] = val;
+            if constexpr (W > 1) x.sc[(PSG_TAG_INIT * PSG_NFIELDS + f) * 64 * W + g.pid] = val;
+          }
+          x.o[f] = c == 0 ? val : x.c[f];
+          x.c[f] = val;
+          if constexpr (W > 1) {
+            x.sc[(PSG_TAG_OLD * PSG_NFIELDS + f) * 64 * W + g.pid] = x.o[f];
+            x.sc[(PSG_TAG_CUR * PSG_NFIELDS + f) * 64 * W + g.pid] = val;
+          }
+        }
         if (c == 0) {
-          x.i[f] = val;
-          if constexpr (W > 1) x.sc[(PSG_TAG_INIT * PSG_NFIELDS + f) * 64 * W + g.pid] = val;
+          if constexpr (S::kInitSet0 >= 0) x.iset[0].build(g, iset_lds(0, grp), x.i[S::kInitSet0]);
+          if constexpr (S::kInitSet1 >= 0) x.iset[1].build(g, iset_lds(1, grp), x.i[S::kInitSet1]);
         }
-        x.o[f] = c == 0 ? val : x.c[f];
-        x.c[f] = val;
-        if constexpr (W > 1) {
-          x.sc[(PSG_TAG_OLD * PSG_NFIELDS + f) * 64 * W + g.pid] = x.o[f];
-          x.sc[(PSG_TAG_CUR * PSG_NFIELDS + f) * 64 * W + g.pid] = val;
-        }
+        if constexpr (W > 1) __syncthreads();
       }
-      if (c == 0) {
-        if constexpr (S::kInitSet0 >= 0) x.iset[0].build(g, iset_lds(0, grp), x.i[S::kInitSet0]);
-        if constexpr (S::kInitSet1 >= 0) x.iset[1].build(g, iset_lds(1, grp), x.i[S::kInitSet1]);
-      }
-      if constexpr (W > 1) __syncthreads();
       uint32_t fb = S::template fail<W>(x, scratch_lds(grp));
       if (c == 0) fb &= ~S::kRelational;
       const bool term = S::kHasTerm && S::template term<W>(x, scratch_lds(grp));
