@@ -1289,6 +1289,7 @@ PSG_DEV void trace_put(const Grp<W>& g, const KArgs& a, uint64_t i, int c, int32
 struct NoHook {
   static constexpr bool kFused = false;
   static constexpr int kSlots = 0;
+  static constexpr uint32_t kFields = 0;  // state fields the hook's Spec reads (psg.h PSG_FIELD_*)
   template <int W>
   struct State {
     Checks ck;

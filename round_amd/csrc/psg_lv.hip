@@ -14,12 +14,6 @@
 #include "psg_device.hpp"
 #include "psg_kernels.hpp"
 
-#ifndef PSG_LV_CHECK_V2
-#define PSG_LV_CHECK_V2 1
-#endif
-#ifndef PSG_LV_EXP
-#define PSG_LV_EXP 0  // timing experiments only (1: no majority scan, 2: check reduced to termination)
-#endif
 
 namespace psg {
 
@@ -51,61 +45,85 @@ PSG_DEV void lv_stage(Grp<W>& g, LvLds<W>& L, int32_t x, int32_t ts, int32_t vot
 // 5 Integrity, 6 Irrevocability. roundInvariants(j-1)(0) is `true` for every j.
 // xin01 / din01: 1 iff x / decision is an initial value (tracked by the round step: x and
 // decision only ever take the coordinator's uniform vote, whose membership is probed once).
+// Scalar-lean form: the kernel is bound by scalar issue, so every "some process" test is one
+// ballot of a per-lane VALU predicate, and the binary search's bookkeeping runs in uniform VGPRs.
+//
+// Split in two: LvState holds every term that reads the process state alone; lv_check_at
+// combines it with the terms that read r and coord (the majority clause, (i.ts == r/4) ==>
+// coord.commit). lv_check = both at one check point; the quiescent tail (lv_body), whose
+// state is final, forms the state terms once and evaluates lv_check_at at each of its check
+// points.
 template <int W>
-PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, int32_t r4, int coord, bool has_old, int n,
-                      const Mask<W>& full, int32_t x, int32_t ts, int32_t vote, int32_t decision, uint32_t fl,
-                      uint32_t old_fl, int32_t old_decision, uint32_t xin01, uint32_t din01) {
-  // r4 = c / 4, coord = (c / 4) % n: maintained incrementally by the caller (a runtime `% n`
-  // is a scalar multiply-high sequence per use on this scalar-issue-bound kernel)
+struct LvState {
+  bool same, keep, validity, irrev, noDec, zAny, zOk, anyD, term;
+  int32_t z0;
+  Mask<W> C;  // processes with commit
+};
+
+// FROZEN: the pre-round state is the current one (quiescent tail), so the Irrevocability witness
+// old.decided && !(decided && old.decision == decision) is 0.
+template <int W, bool FROZEN = false>
+PSG_DEV LvState<W> lv_state(Grp<W>& g, LvLds<W>& L, bool has_old, const Mask<W>& full, int32_t x, int32_t ts,
+                            int32_t vote, int32_t decision, uint32_t fl, uint32_t old_fl, int32_t old_decision,
+                            uint32_t xin01, uint32_t din01) {
   lv_stage<W>(g, L, x, ts, vote, decision);
-#if PSG_LV_CHECK_V2
-  // Scalar-lean form: the kernel is bound by scalar issue (SALU 0.94 of one per cycle per CU),
-  // so every "some process" test is one ballot of a per-lane VALU predicate, and the
-  // binary search's bookkeeping runs in uniform VGPRs; the formulas are those of the
-  // reference form below (kept for A/B: -DPSG_LV_CHECK_V2=0).
+  LvState<W> st;
   const uint32_t dec01 = fl & F_DECIDED;  // F_DECIDED == 1
   const Mask<W> D = g.ballot_any(dec01 != 0u);  // never set past n
-  const bool anyD = many(D);
-  const int32_t d0 = anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
-  if (PSG_LV_EXP == 2) { ck.record(0, meq(D, full), c, g.lane); return; }
+  st.anyD = many(D);
+  st.term = meq(D, full);
+  const int32_t d0 = st.anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
   // Agreement, keepInit, Validity and Irrevocability from one ballot of a per-process
   // witness word (decision != d0; x or a decision not initial; a changed decision),
   // resolved formula by formula only when some process is a witness
   uint32_t wit = (dec01 & (ne01(decision, d0) | (1u - din01))) | (1u - xin01);
-  if (has_old) wit |= (old_fl & F_DECIDED) & (1u - (dec01 & eq01(old_decision, decision)));
-  bool same = true, keep = true, validity = true, irrev = true;
+  if (has_old && !FROZEN) wit |= (old_fl & F_DECIDED) & (1u - (dec01 & eq01(old_decision, decision)));
+  st.same = st.keep = st.validity = st.irrev = true;
   if (g.any_raw(wit != 0u)) {  // wit, dec01, old_fl & F_DECIDED are 0 past n
-    same = !g.any_raw(dec01 != 0u && decision != d0);
-    keep = !g.any(xin01 == 0u);  // P.forall(i => P.exists(j1 => i.x == init(j1.x)))
-    validity = !g.any_raw(dec01 != 0u && din01 == 0u);
-    irrev = !has_old || !g.any_raw((old_fl & F_DECIDED) != 0u && !(dec01 != 0u && old_decision == decision));
+    st.same = !g.any_raw(dec01 != 0u && decision != d0);
+    st.keep = !g.any(xin01 == 0u);  // P.forall(i => P.exists(j1 => i.x == init(j1.x)))
+    st.validity = !g.any_raw(dec01 != 0u && din01 == 0u);
+    if constexpr (!FROZEN)
+      st.irrev = !has_old || !g.any_raw((old_fl & F_DECIDED) != 0u && !(dec01 != 0u && old_decision == decision));
   }
-  const bool noDec = !g.any_raw((fl & (F_DECIDED | F_READY)) != 0u);  // flags are 0 past n but F_HALTED
+  st.noDec = !g.any_raw((fl & (F_DECIDED | F_READY)) != 0u);  // flags are 0 past n but F_HALTED
   // values pinned by (decided ==> decision == v), (commit ==> vote == v), (ready ==> vote == v):
   // z0 = the pinned value of the first pinned process (its decision if it decided, else its
   // vote), and every pinned process must agree with it
   const uint32_t cr01 = (fl & (F_COMMIT | F_READY)) ? 1u : 0u;
   const Mask<W> Pm = g.ballot_any((dec01 | cr01) != 0u);
-  const bool zAny = many(Pm);
-  int32_t z0 = 0;
-  bool zOk = true;
-  if (zAny) {
+  st.zAny = many(Pm);
+  st.z0 = 0;
+  st.zOk = true;
+  if (st.zAny) {
     const int32_t zl = dec01 ? decision : vote;
     if constexpr (W > 1) {
       L.votes[g.pid] = zl;  // the staged votes are not read after this point of the check
       __syncthreads();
     }
-    z0 = g.bcast(zl, L.votes, mfirst(Pm));
-    zOk = !g.any_raw(((dec01 & ne01(decision, z0)) | (cr01 & ne01(vote, z0))) != 0u);
+    st.z0 = g.bcast(zl, L.votes, mfirst(Pm));
+    st.zOk = !g.any_raw(((dec01 & ne01(decision, st.z0)) | (cr01 & ne01(vote, st.z0))) != 0u);
   }
+  st.C = g.ballot_any((fl & F_COMMIT) != 0u);
+  return st;
+}
+
+template <int W>
+PSG_DEV void lv_check_at(Grp<W>& g, LvLds<W>& L, Checks& ck, const LvState<W>& st, int c, int32_t r4, int coord,
+                         int n, int32_t x, int32_t ts) {
+  // r4 = c / 4, coord = (c / 4) % n: maintained incrementally by the caller (a runtime `% n`
+  // is a scalar multiply-high sequence per use on this scalar-issue-bound kernel)
   bool maj = false;
   // (Invariant0 reads maj only when keepInit holds and some process decided or is ready)
-  if (PSG_LV_EXP != 1 && c > 0 && zOk && keep && !noDec &&
+  if (c > 0 && st.zOk && st.keep && !st.noDec &&
       // (i.ts == r/4) ==> coord.commit
-      (mtest(g.ballot_any((fl & F_COMMIT) != 0u), coord) || !g.any_raw(ts == r4))) {  // ts = -1 past n
+      (mtest(st.C, coord) || !g.any_raw(ts == r4))) {  // ts = -1 past n
     // exists t <= r/4: A_t = {i : i.ts >= t}, |A_t| > n/2, all x over A_t equal (to the pinned
-    // value): the largest u with |{tv >= u}| > n/2 for tv = min(ts, r/4) + 1 (see below), by
-    // binary search; ceil(log2(r/4 + 2)) = bit length of r/4 + 1 steps (a step after
+    // value). The sets A_t shrink as t grows, and "all x over A equal (to z0)" holds on every
+    // non-empty subset of a set it holds on, so the exists holds iff it holds at the largest
+    // t <= r/4 with |A_t| > n/2. With tv = min(ts, r/4) + 1 in [0, r/4 + 1] that is the
+    // largest u with |{tv >= u}| > n/2 (a present value; u = 0 always qualifies): a binary
+    // search on the count, ceil(log2(r/4 + 2)) = bit length of r/4 + 1 steps (a step after
     // convergence keeps lo), lo / hi / mid as uniform VGPR values (vector issue)
     const int32_t tsc = ts < r4 ? ts : r4;
     const uint32_t tv = (uint32_t)(tsc + 1);  // ts >= -1 (LastVoting.scala:87)
@@ -120,75 +138,24 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, int32_t r4, int
     }
     const Mask<W> A = g.ballot(tv >= lo);
     const int32_t xv = g.bcast(x, L.xs, mfirst(A));
-    maj = !g.any(tv >= lo && x != xv) && (!zAny || xv == z0);
+    maj = !g.any(tv >= lo && x != xv) && (!st.zAny || xv == st.z0);
   }
-#else
-  const uint32_t dec01 = (fl & F_DECIDED) ? 1u : 0u;
-  const Mask<W> D = g.ballot(dec01 != 0u);
-  const Mask<W> C = g.ballot((fl & F_COMMIT) != 0u);
-  const Mask<W> Rd = g.ballot((fl & F_READY) != 0u);
-  const bool anyD = many(D);
-  const int32_t d0 = anyD ? g.bcast(decision, L.ds, mfirst(D)) : 0;
-  if (PSG_LV_EXP == 2) { ck.record(0, meq(D, full), c, g.lane); return; }
-  // Agreement, keepInit, Validity and Irrevocability from one ballot of a per-process
-  // witness word (decision != d0; x or a decision not initial; a changed decision),
-  // resolved formula by formula only when some process is a witness
-  uint32_t wit = (dec01 & (ne01(decision, d0) | (1u - din01))) | (1u - xin01);
-  if (has_old) wit |= ((old_fl & F_DECIDED) ? 1u : 0u) & (1u - (dec01 & eq01(old_decision, decision)));
-  bool same = true, keep = true, validity = true, irrev = true;
-  if (g.any(wit != 0u)) {
-    same = !many(mand(D, g.ballot(decision != d0)));
-    keep = !many(mand(full, g.ballot(xin01 == 0u)));  // P.forall(i => P.exists(j1 => i.x == init(j1.x)))
-    validity = !many(mand(D, g.ballot(din01 == 0u)));
-    const Mask<W> OLD = g.ballot((old_fl & F_DECIDED) != 0u);
-    irrev = !has_old || !many(mandn(OLD, mand(D, g.ballot(old_decision == decision))));
-  }
-  const bool noDec = !many(mor(D, Rd));
-  // values pinned by (decided ==> decision == v), (commit ==> vote == v), (ready ==> vote == v)
-  const Mask<W> CR = mor(C, Rd);
-  const Mask<W> Pm = mor(D, CR);
-  const bool zAny = many(Pm);
-  int32_t z0 = 0;
-  bool zOk = true;
-  if (zAny) {
-    const int q = mfirst(Pm);
-    const bool qD = mtest(D, q);  // then q is also the first decider: z0 = d0
-    z0 = qD ? d0 : g.bcast(vote, L.votes, q);
-    // the deciders' part is empty when every decision equals d0 = z0 (or nobody decided)
-    const Mask<W> zd = (same && (qD || !anyD)) ? mzero<W>() : mand(D, g.ballot(decision != z0));
-    zOk = !many(mor(zd, mand(CR, g.ballot(vote != z0))));
-  }
-  const bool c5 = mtest(C, coord) || !g.any(ts == r4);  // (i.ts == r/4) ==> coord.commit
-  bool maj = false;
-  // (Invariant0 reads maj only when keepInit holds and some process decided or is ready)
-  if (PSG_LV_EXP != 1 && c > 0 && zOk && c5 && keep && !noDec) {
-    // exists t <= r/4: A_t = {i : i.ts >= t}, |A_t| > n/2, all x over A_t equal (to the pinned
-    // value). The sets A_t shrink as t grows, and "all x over A equal (to z0)" holds on every
-    // non-empty subset of a set it holds on, so the exists holds iff it holds at the largest
-    // t <= r/4 with |A_t| > n/2. With tv = min(ts, r/4) + 1 in [0, r/4 + 1] that is the
-    // largest u with |{tv >= u}| > n/2 (a present value; u = 0 always qualifies): a binary
-    // search on the count, ceil(log2(r/4 + 2)) ballots.
-    const int32_t tsc = ts < r4 ? ts : r4;
-    const uint32_t tv = (uint32_t)(tsc + 1);  // ts >= -1 (LastVoting.scala:87)
-    uint32_t lo = 0, hi = (uint32_t)r4 + 2u;
-    while (hi - lo > 1u) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (mpopc(g.ballot(tv >= mid)) > n / 2) lo = mid;
-      else hi = mid;
-    }
-    const Mask<W> A = g.ballot(tv >= lo);
-    const int32_t xv = g.bcast(x, L.xs, mfirst(A));
-    maj = !many(mand(A, g.ballot(x != xv))) && (!zAny || xv == z0);
-  }
-#endif
-  const bool inv0 = keep && (noDec || maj);
-  const bool d0in = same && validity;
-  const bool term = meq(D, full);
-  const bool inv1 = term && d0in;
-  const bool integrity = !anyD || d0in;
-  const uint32_t fb = fbit(inv0 || inv1, 0) | fbit(inv0, 1) | fbit(inv1, 2) | fbit(same, 3) | fbit(validity, 4) |
-                      fbit(integrity, 5) | fbit(irrev, 6);
-  ck.record(fb, term, c, g.lane);
+  const bool inv0 = st.keep && (st.noDec || maj);
+  const bool d0in = st.same && st.validity;
+  const bool inv1 = st.term && d0in;
+  const bool integrity = !st.anyD || d0in;
+  const uint32_t fb = fbit(inv0 || inv1, 0) | fbit(inv0, 1) | fbit(inv1, 2) | fbit(st.same, 3) |
+                      fbit(st.validity, 4) | fbit(integrity, 5) | fbit(st.irrev, 6);
+  ck.record(fb, st.term, c, g.lane);
+}
+
+template <int W>
+PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, int32_t r4, int coord, bool has_old, int n,
+                      const Mask<W>& full, int32_t x, int32_t ts, int32_t vote, int32_t decision, uint32_t fl,
+                      uint32_t old_fl, int32_t old_decision, uint32_t xin01, uint32_t din01) {
+  const LvState<W> st =
+      lv_state<W>(g, L, has_old, full, x, ts, vote, decision, fl, old_fl, old_decision, xin01, din01);
+  lv_check_at<W>(g, L, ck, st, c, r4, coord, n, x, ts);
 }
 
 // The coordinator's HO mask (uniform).
@@ -289,9 +256,9 @@ PSG_DEV void lv_body(const KArgs& a) {
     ck.reset();
     typename SH::template State<W> sh(g, grp, n);  // fused Spec evaluation state (NoHook: empty)
     if constexpr (!SH::kFused) lv_check<W>(g, L, ck, 0, 0, 0, false, n, full, x, ts, vote, decision, fl, 0u, -1, xin, din);
-    auto trace = [&](int c, int32_t hs) {
+    auto trace = [&](int c, int32_t hs, bool frozen = false) {
       emit_state<W, SH>(sh, g, a, i, c, x, (fl & F_DECIDED) ? 1 : 0, decision, ts, (fl & F_READY) ? 1 : 0,
-                   (fl & F_COMMIT) ? 1 : 0, vote, 0, hs);
+                        (fl & F_COMMIT) ? 1 : 0, vote, 0, hs, frozen);
     };
     if (tracing<SH>(a)) trace(0, n);
     pt.mark(0);
@@ -388,7 +355,25 @@ PSG_DEV void lv_body(const KArgs& a) {
       if (tracing<SH>(a)) trace(k + 1, (old_fl & F_HALTED) ? n : hs);
       pt.mark(many(act) ? 4 : 5);
     };
+    // Quiescent tail. At a phase boundary past round 0, once at most n/2 processes are not halted
+    // and none of them is commit or ready, no process can take an effective step again: R0's
+    // commit needs a mailbox of more than n/2 (LastVoting.scala:129), R2's ready more than n/2
+    // (177; the unmutated quorum), R1 / R3 send only from a commit / ready coordinator (141,
+    // 187), and R3's reset finds the flags already clear — so the state, old included, is final.
+    // Rounds kq .. R-1 then draw no HO set and run no step; every check point is still evaluated
+    // (the Spec reads r / coord). Not taken when a trace or the fused Spec reads |mailbox|.
+    const bool hs_read = SH::kFused ? ((SH::kFields >> PSG_FIELD_HOSIZE) & 1u) != 0u
+                                    : (a.trace != nullptr && ((a.trace_fields >> PSG_FIELD_HOSIZE) & 1u));
+    const bool qok = a.variant == 0 && !hs_read;
+    int kq = a.R;
     for (int k0 = 0; k0 < a.R; k0 += 4) {
+      if (qok && k0 > 0) {
+        const Mask<W> live = g.ballot_any((fl & F_HALTED) == 0u);  // lanes past n are halted
+        if (2 * mpopc(live) <= n && !g.any_raw((fl & F_HALTED) == 0u && (fl & (F_COMMIT | F_READY)) != 0u)) {
+          kq = k0;
+          break;
+        }
+      }
       round(k0, Slot<0>{});
       if (k0 + 1 < a.R) round(k0 + 1, Slot<1>{});
       if (k0 + 2 < a.R) round(k0 + 2, Slot<2>{});
@@ -396,6 +381,21 @@ PSG_DEV void lv_body(const KArgs& a) {
       ++phase;
       cph = cnx;
       cnx = cnx + 1 == n ? 0 : cnx + 1;
+    }
+    LvState<W> st;
+    if (!SH::kFused && kq < a.R)
+      st = lv_state<W, true>(g, L, true, full, x, ts, vote, decision, fl, fl, decision, xin, din);
+    for (int k = kq; k < a.R; ++k) {
+      const int RS = k & 3;
+      if constexpr (!SH::kFused)
+        lv_check_at<W>(g, L, ck, st, k + 1, RS == 3 ? phase + 1 : phase, RS == 3 ? cnx : cph, n, x, ts);
+      if (tracing<SH>(a)) trace(k + 1, n, true);
+      if (RS == 3) {
+        ++phase;
+        cph = cnx;
+        cnx = cnx + 1 == n ? 0 : cnx + 1;
+      }
+      pt.mark(5);
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 7, dec_val, dec_round, halt_round, x, &bc);
     pt.mark(3);

@@ -668,6 +668,7 @@ template <class S>
 struct SpecHook {
   static constexpr bool kFused = true;
   static constexpr int kSlots = S::kSlots;
+  static constexpr uint32_t kFields = S::kFields;
   template <int W>
   struct State {
     Ctx<W> x;
