@@ -104,8 +104,9 @@ PSG_DEV void slv_body(const KArgs& a) {
       kagree_check<W>(g, ck, c, 1, full, (fl & S_DECIDED) != 0u, decision, X0, false, L.ds);
     };
     if constexpr (!SH::kFused) check(0);
-    auto trace = [&](int c, int32_t hs) {
-      emit_state<W, SH>(sh, g, a, i, c, x, (fl & S_DECIDED) ? 1 : 0, decision, ts, 0, (fl & S_COMMIT) ? 1 : 0, vote, 0, hs);
+    auto trace = [&](int c, int32_t hs, bool frozen = false) {
+      emit_state<W, SH>(sh, g, a, i, c, x, (fl & S_DECIDED) ? 1 : 0, decision, ts, 0, (fl & S_COMMIT) ? 1 : 0, vote, 0, hs,
+                        frozen);
     };
     if (tracing<SH>(a)) trace(0, n);
 
@@ -185,10 +186,32 @@ PSG_DEV void slv_body(const KArgs& a) {
       if constexpr (!SH::kFused) check(k + 1);
       if (tracing<SH>(a)) trace(k + 1, (fl_start & S_HALTED) ? n : hs);
     };
+    // Quiescent tail (as lv_body's). At a phase boundary, once at most n/2 processes are not
+    // halted and none of them is commit, no process can take an effective step again: R0's
+    // commit needs a mailbox of more than n/2 (ShortLastVoting.scala:39), R2's decision more
+    // than n/2 (85; the unmutated quorum), R1 sends only from a commit coordinator (53), and R2's
+    // reset finds the flag clear — the state is final. Rounds kq .. R-1 then draw no HO set and
+    // run no step; the check is still evaluated at every check point. Not taken when a trace or
+    // the fused Spec reads |mailbox|.
+    const bool hs_read = SH::kFused ? ((SH::kFields >> PSG_FIELD_HOSIZE) & 1u) != 0u
+                                    : (a.trace != nullptr && ((a.trace_fields >> PSG_FIELD_HOSIZE) & 1u));
+    const bool qok = a.variant == 0 && !hs_read;
+    int kq = a.R;
     for (int k0 = 0; k0 < a.R; k0 += 3) {
+      if (qok && k0 > 0) {
+        const Mask<W> live = g.ballot((fl & S_HALTED) == 0u);
+        if (2 * mpopc(live) <= n && !g.any((fl & (S_HALTED | S_COMMIT)) == S_COMMIT)) {
+          kq = k0;
+          break;
+        }
+      }
       round(k0, Slot<0>{});
       if (k0 + 1 < a.R) round(k0 + 1, Slot<1>{});
       if (k0 + 2 < a.R) round(k0 + 2, Slot<2>{});
+    }
+    for (int k = kq; k < a.R; ++k) {
+      if constexpr (!SH::kFused) check(k + 1);
+      if (tracing<SH>(a)) trace(k + 1, n, true);
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 2, dec_val, dec_round, halt_round, x, &bc);
   }
