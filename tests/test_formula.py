@@ -46,7 +46,9 @@ def test_custom_specs_match_direct_evaluation(cid, alg, n, kw, mk, oracle_mod):
     cfg = psync.make_config(alg, n, seed=17, **kw)
     spec = mk()
     prog = F.compile_spec(spec, alg.alg_id)
-    cnt = 12
+    # the direct evaluation brute-forces nested V.exists domains in Python: fewer instances for the
+    # larger / nested cases keeps the CPU suite within minutes
+    cnt = 12 if n <= 12 and not cid.startswith("lv") else 4
     tr = oracle_mod.trace(cfg, 0, cnt)
     ff, tm = oracle_mod.vm_run(prog, tr, cnt, n, cfg.rounds)
     rf, rt = formula_ref.evaluate(spec, tr, cnt, n, cfg.rounds)
