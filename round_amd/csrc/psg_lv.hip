@@ -48,11 +48,9 @@ PSG_DEV void lv_stage(Grp<W>& g, LvLds<W>& L, int32_t x, int32_t ts, int32_t vot
 // Scalar-lean form: the kernel is bound by scalar issue, so every "some process" test is one
 // ballot of a per-lane VALU predicate, and the binary search's bookkeeping runs in uniform VGPRs.
 //
-// Split in two: LvState holds every term that reads the process state alone; lv_check_at
+// In two parts: LvState holds every term that reads the process state alone; lv_check_at
 // combines it with the terms that read r and coord (the majority clause, (i.ts == r/4) ==>
-// coord.commit). lv_check = both at one check point; the quiescent tail (lv_body), whose
-// state is final, forms the state terms once and evaluates lv_check_at at each of its check
-// points.
+// coord.commit). lv_check = both, at every check point (the quiescent tail's too).
 template <int W>
 struct LvState {
   bool same, keep, validity, irrev, noDec, zAny, zOk, anyD, term;
@@ -60,8 +58,9 @@ struct LvState {
   Mask<W> C;  // processes with commit
 };
 
-// FROZEN: the pre-round state is the current one (quiescent tail), so the Irrevocability witness
-// old.decided && !(decided && old.decision == decision) is 0.
+// FROZEN: a check point of the quiescent tail (lv_body): the pre-round state is the current one, so
+// the Irrevocability witness old.decided && !(decided && old.decision == decision) is 0, and no
+// process is commit or ready (the tail's condition), so those flags' terms are 0.
 template <int W, bool FROZEN = false>
 PSG_DEV LvState<W> lv_state(Grp<W>& g, LvLds<W>& L, bool has_old, const Mask<W>& full, int32_t x, int32_t ts,
                             int32_t vote, int32_t decision, uint32_t fl, uint32_t old_fl, int32_t old_decision,
@@ -86,11 +85,11 @@ PSG_DEV LvState<W> lv_state(Grp<W>& g, LvLds<W>& L, bool has_old, const Mask<W>&
     if constexpr (!FROZEN)
       st.irrev = !has_old || !g.any_raw((old_fl & F_DECIDED) != 0u && !(dec01 != 0u && old_decision == decision));
   }
-  st.noDec = !g.any_raw((fl & (F_DECIDED | F_READY)) != 0u);  // flags are 0 past n but F_HALTED
+  st.noDec = !g.any_raw((fl & (FROZEN ? F_DECIDED : F_DECIDED | F_READY)) != 0u);  // 0 past n but F_HALTED
   // values pinned by (decided ==> decision == v), (commit ==> vote == v), (ready ==> vote == v):
   // z0 = the pinned value of the first pinned process (its decision if it decided, else its
   // vote), and every pinned process must agree with it
-  const uint32_t cr01 = (fl & (F_COMMIT | F_READY)) ? 1u : 0u;
+  const uint32_t cr01 = !FROZEN && (fl & (F_COMMIT | F_READY)) ? 1u : 0u;
   const Mask<W> Pm = g.ballot_any((dec01 | cr01) != 0u);
   st.zAny = many(Pm);
   st.z0 = 0;
@@ -104,7 +103,7 @@ PSG_DEV LvState<W> lv_state(Grp<W>& g, LvLds<W>& L, bool has_old, const Mask<W>&
     st.z0 = g.bcast(zl, L.votes, mfirst(Pm));
     st.zOk = !g.any_raw(((dec01 & ne01(decision, st.z0)) | (cr01 & ne01(vote, st.z0))) != 0u);
   }
-  st.C = g.ballot_any((fl & F_COMMIT) != 0u);
+  st.C = FROZEN ? mzero<W>() : g.ballot_any((fl & F_COMMIT) != 0u);
   return st;
 }
 
@@ -149,12 +148,12 @@ PSG_DEV void lv_check_at(Grp<W>& g, LvLds<W>& L, Checks& ck, const LvState<W>& s
   ck.record(fb, st.term, c, g.lane);
 }
 
-template <int W>
+template <int W, bool FROZEN = false>
 PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, int32_t r4, int coord, bool has_old, int n,
                       const Mask<W>& full, int32_t x, int32_t ts, int32_t vote, int32_t decision, uint32_t fl,
                       uint32_t old_fl, int32_t old_decision, uint32_t xin01, uint32_t din01) {
   const LvState<W> st =
-      lv_state<W>(g, L, has_old, full, x, ts, vote, decision, fl, old_fl, old_decision, xin01, din01);
+      lv_state<W, FROZEN>(g, L, has_old, full, x, ts, vote, decision, fl, old_fl, old_decision, xin01, din01);
   lv_check_at<W>(g, L, ck, st, c, r4, coord, n, x, ts);
 }
 
@@ -356,12 +355,13 @@ PSG_DEV void lv_body(const KArgs& a) {
       pt.mark(many(act) ? 4 : 5);
     };
     // Quiescent tail. At a phase boundary past round 0, once at most n/2 processes are not halted
-    // and none of them is commit or ready, no process can take an effective step again: R0's
+    // and no process is commit or ready, no process can take an effective step again: R0's
     // commit needs a mailbox of more than n/2 (LastVoting.scala:129), R2's ready more than n/2
     // (177; the unmutated quorum), R1 / R3 send only from a commit / ready coordinator (141,
     // 187), and R3's reset finds the flags already clear — so the state, old included, is final.
-    // Rounds kq .. R-1 then draw no HO set and run no step; every check point is still evaluated
-    // (the Spec reads r / coord). Not taken when a trace or the fused Spec reads |mailbox|.
+    // Rounds kq .. R-1 then draw no HO set and run no step; the Spec is still evaluated at every
+    // check point (with old = current: the Irrevocability witness is 0 by algebra, as in OTR's
+    // frozen tail). Not taken when a trace or the fused Spec reads |mailbox|.
     const bool hs_read = SH::kFused ? ((SH::kFields >> PSG_FIELD_HOSIZE) & 1u) != 0u
                                     : (a.trace != nullptr && ((a.trace_fields >> PSG_FIELD_HOSIZE) & 1u));
     const bool qok = a.variant == 0 && !hs_read;
@@ -369,7 +369,7 @@ PSG_DEV void lv_body(const KArgs& a) {
     for (int k0 = 0; k0 < a.R; k0 += 4) {
       if (qok && k0 > 0) {
         const Mask<W> live = g.ballot_any((fl & F_HALTED) == 0u);  // lanes past n are halted
-        if (2 * mpopc(live) <= n && !g.any_raw((fl & F_HALTED) == 0u && (fl & (F_COMMIT | F_READY)) != 0u)) {
+        if (2 * mpopc(live) <= n && !g.any_raw((fl & (F_COMMIT | F_READY)) != 0u)) {
           kq = k0;
           break;
         }
@@ -382,13 +382,11 @@ PSG_DEV void lv_body(const KArgs& a) {
       cph = cnx;
       cnx = cnx + 1 == n ? 0 : cnx + 1;
     }
-    LvState<W> st;
-    if (!SH::kFused && kq < a.R)
-      st = lv_state<W, true>(g, L, true, full, x, ts, vote, decision, fl, fl, decision, xin, din);
     for (int k = kq; k < a.R; ++k) {
       const int RS = k & 3;
       if constexpr (!SH::kFused)
-        lv_check_at<W>(g, L, ck, st, k + 1, RS == 3 ? phase + 1 : phase, RS == 3 ? cnx : cph, n, x, ts);
+        lv_check<W, true>(g, L, ck, k + 1, RS == 3 ? phase + 1 : phase, RS == 3 ? cnx : cph, true, n, full, x, ts,
+                          vote, decision, fl, fl, decision, xin, din);
       if (tracing<SH>(a)) trace(k + 1, n, true);
       if (RS == 3) {
         ++phase;
