@@ -174,6 +174,9 @@ PSG_DEV void otr_body(const KArgs& a) {
     if (tracing_on) trace(0, n);
     pt.mark(0);
 
+    // does a trace or the fused Spec read |mailbox| (psg.h PSG_FIELD_HOSIZE)?
+    const bool hs_needed = SH::kFused ? ((SH::kFields >> PSG_FIELD_HOSIZE) & 1u) != 0u
+                                      : (TR && a.trace != nullptr && ((a.trace_fields >> PSG_FIELD_HOSIZE) & 1u));
     int32_t live_rounds = 0;  // rounds in which some process took a step
     int kf = a.R;             // first round in which every process had halted (the state is final)
     for (int k = 0; k < a.R; ++k) {
@@ -187,6 +190,21 @@ PSG_DEV void otr_body(const KArgs& a) {
       }
       {
         live_rounds = k + 1;
+        // Settled round: every live process has decided d and holds x = d. Then every mailbox
+        // holds only d, so mmor is d (OtrExample.scala:67-75) and a mailbox above 2n/3 re-decides
+        // the d it holds (Otr.scala:63-73): no process's x, decision or decided changes whatever
+        // its HO set is, and only `after` counts down (Otr.scala:75-80). The round's HO sets are
+        // then not drawn and mmor not run (the schedule is a pure function of (instance, round,
+        // pid), so no other draw moves); the check point after it is evaluated as every other.
+        // Not taken when a trace or the fused Spec reads |mailbox|.
+        bool settled = false;
+        if constexpr (W == 1) {
+          if (!hs_needed) {
+            const int32_t d0 = readlane32(decision, mfirst(act));
+            settled = !g.any_raw(halted01 == 0u && !(dec01 != 0u && decision == d0 && x == d0));
+          }
+        }
+        if (!settled) {
         Mask<W> goodS;
         const bool good = sc.good_round(k, g.lane, a.R, goodS);
         Mask<W> CB = mzero<W>(), CN = mzero<W>();
@@ -257,6 +275,7 @@ PSG_DEV void otr_body(const KArgs& a) {
           dec01 |= newdec;
           if constexpr (!SH::kFused) X0.maybe_out01_2(decision, x, od, ox);
         }
+        }  // !settled
         // after -= 1 once decided; exitAtEndOfRound when it reaches 0 (Otr.scala:75-80)
         const uint32_t ad = (1u - halted01) & dec01;
         after -= (int32_t)ad;
