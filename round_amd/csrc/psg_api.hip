@@ -218,7 +218,9 @@ static KArgs make_args(const psg_ctx* c) {
   a.drop_log2 = f.sched.drop_log2;
   a.good_p32 = f.sched.good_p32;
   a.good_min = f.sched.good_min;
-  a.crash_fmax = f.sched.crash_fmax;
+  // at most 0 crashes: f = mulhi32(w, fmax + 1) = 0 for every instance, so nobody crashes — the
+  // kernels skip the instance's crash draws and the per-round crash sets (the same schedule)
+  a.crash_fmax = f.sched.crash_fmax == 0 ? -1 : f.sched.crash_fmax;
   a.ho_min = f.sched.ho_min;
   a.self_bit = f.sched.self_bit;
   a.counters = c->d_counters;
