@@ -46,34 +46,103 @@ struct EpsLds {
   double sx[Geometry<W>::kGroups][64 * W];
   int32_t spid[Geometry<W>::kGroups][64 * W];
   int64_t keys[W > 1 ? 64 * W : 1];
+  uint8_t sel8[W == 1 ? 256 * 8 : 1];  // W = 1: sel8[v * 8 + r] = bit index of the r-th set bit of byte v
+};
+
+// per-byte popcounts of a 32-bit word (each byte of the result: 0..8)
+PSG_DEV uint32_t bytepop(uint32_t v) {
+  v = v - ((v >> 1) & 0x55555555u);
+  v = (v & 0x33333333u) + ((v >> 2) & 0x33333333u);
+  return (v + (v >> 4)) & 0x0F0F0F0Fu;
+}
+
+// Rank select over a 64-bit member mask (W = 1): the position of its j-th set bit (0-based,
+// j < popcount), from per-byte prefix counts instead of dropping the j lowest bits one by one.
+// cum_* byte b = set bits in bytes 0..b of that half (<= 32, so the SWAR compare below cannot
+// borrow across bytes); the byte holding the target is the number of bytes whose prefix count
+// is <= j, and the bit inside it comes from the sel8 table.
+struct RankSel {
+  uint32_t w[2], cum[2], nlo;
+  PSG_DEV explicit RankSel(uint64_t m) {
+    w[0] = (uint32_t)m;
+    w[1] = (uint32_t)(m >> 32);
+    cum[0] = bytepop(w[0]) * 0x01010101u;
+    cum[1] = bytepop(w[1]) * 0x01010101u;
+    nlo = cum[0] >> 24;
+  }
+  PSG_DEV int at(uint32_t j, const uint8_t* sel8) const {
+    const bool hi = j >= nlo;
+    const uint32_t r = hi ? j - nlo : j;
+    const uint32_t c = hi ? cum[1] : cum[0];
+    const uint32_t v = hi ? w[1] : w[0];
+    const uint32_t ge = ((c | 0x80808080u) - (r + 1u) * 0x01010101u) & 0x80808080u;  // bytes with prefix > r
+    const uint32_t b8 = (4u - (uint32_t)__builtin_popcount(ge)) * 8u;                  // target byte * 8
+    const uint32_t before = (c << 8) >> b8 & 0xFFu;                                    // prefix of the bytes below
+    const uint32_t byte = (v >> b8) & 0xFFu;
+    return (hi ? 32 : 0) + (int)b8 + sel8[byte * 8u + (r - before)];
+  }
 };
 
 // Ascending bitonic sort of (key, pid) pairs over the 64 lanes of a wave (pairs must
-// be distinct; pids are). Stage (size, d): partners lane ^ d exchange through the LDS
-// crossbar; the lower lane of a pair keeps the smaller pair in an ascending block.
-template <int SIZE, int D>
-PSG_DEV void sort_stage(int64_t& key, int32_t& pid, int lane) {
-  const int64_t pk = (int64_t)xshfl64<D>((uint64_t)key, lane);
-  const int32_t pp = (int32_t)xshfl<D>((uint32_t)pid, lane);
+// be distinct; pids are), in the all-ascending form: each merge of two sorted blocks of
+// SIZE/2 starts by pairing lane l with its mirror l ^ (SIZE - 1), then half-cleans with
+// partners l ^ D, D = SIZE/4 .. 1; in every step the lower lane of a pair keeps the smaller
+// pair. The upper-lane test is one lane bit (6 distinct masks over the 21 steps, instead of
+// 21 direction masks that do not fit the SGPRs).
+// lane l receives lane l ^ X's v. Within a quad (X = 1, 2, 3) and the mirrors of a half row
+// / row (X = 7, 15) one DPP move; the rest through the LDS crossbar (ds_bpermute). The sort
+// is a chain of 21 dependent exchanges, so exchange latency, not issue, sets its cost: the
+// DPP moves took the W2 row 11.65 -> 10.92 ms; X = 4, 8 as a DPP row shift each way and a
+// select (11.54), and X = 16, 31, 63 by v_permlane16/32_swap (11.50) measured slower.
+template <int CTRL>
+PSG_DEV uint32_t dpp_mov(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false); }
+template <int X>
+PSG_DEV uint32_t xchg(uint32_t v) {
+  if constexpr (X == 1) return dpp_mov<0xB1>(v);          // quad_perm [1,0,3,2]
+  else if constexpr (X == 2) return dpp_mov<0x4E>(v);     // quad_perm [2,3,0,1]
+  else if constexpr (X == 3) return dpp_mov<0x1B>(v);     // quad_perm [3,2,1,0]
+  else if constexpr (X == 7) return dpp_mov<0x141>(v);    // row_half_mirror
+  else if constexpr (X == 15) return dpp_mov<0x140>(v);   // row_mirror
+  else return (uint32_t)__shfl_xor((int)v, X);
+}
+template <int X>
+PSG_DEV uint64_t xchg64(uint64_t v) {
+  return (uint64_t)xchg<X>((uint32_t)v) | ((uint64_t)xchg<X>((uint32_t)(v >> 32)) << 32);
+}
+template <int X, int UP>
+PSG_DEV void sort_step(int64_t& key, int32_t& pid, int lane) {
+  const int64_t pk = (int64_t)xchg64<X>((uint64_t)key);
+  const int32_t pp = (int32_t)xchg<X>((uint32_t)pid);
   const bool less = pk < key || (pk == key && pp < pid);  // partner's pair precedes mine
-  const bool take = less != (((lane & D) != 0) != ((lane & SIZE) != 0));
+  const bool take = less != ((lane & UP) != 0);
   key = take ? pk : key;
   pid = take ? pp : pid;
-  if constexpr (D > 1) sort_stage<SIZE, D / 2>(key, pid, lane);
+}
+template <int D>
+PSG_DEV void half_clean(int64_t& key, int32_t& pid, int lane) {
+  sort_step<D, D>(key, pid, lane);
+  if constexpr (D > 1) half_clean<D / 2>(key, pid, lane);
 }
 template <int SIZE = 2>
 PSG_DEV void wave_sort_key_pid(int64_t& key, int32_t& pid, int lane) {
-  sort_stage<SIZE, SIZE / 2>(key, pid, lane);  // partners exchange in registers (xshfl)
+  sort_step<SIZE - 1, SIZE / 2>(key, pid, lane);  // mirror step
+  if constexpr (SIZE >= 4) half_clean<SIZE / 4>(key, pid, lane);
   if constexpr (SIZE < 64) wave_sort_key_pid<SIZE * 2>(key, pid, lane);
 }
 
 // 64 x 64 bit-matrix transpose across a wave: lane i holds row i; afterwards lane j holds
 // column j (bit i = bit j of row i). The six swap stages of the block transpose: at stage
 // s, the lane pair (i, i ^ s) exchanges the off-diagonal s x s blocks of its 2s x 2s block.
+// Branch-free: the upper lane of a pair keeps its ~LO blocks and takes the partner's ~LO
+// blocks shifted down into LO, the lower lane the mirror image (two selects and two bitfield
+// inserts instead of a divergent if / else).
 template <int S, uint64_t LO>
 PSG_DEV uint64_t transpose_stage(uint64_t r, int lane) {
   const uint64_t p = xshfl64<S>(r, lane);
-  return (lane & S) ? ((r & ~LO) | ((p & ~LO) >> S)) : ((r & LO) | ((p & LO) << S));
+  const bool up = (lane & S) != 0;
+  const uint64_t keep = up ? ~LO : LO;
+  const uint64_t moved = up ? (p >> S) : (p << S);
+  return (r & keep) | (moved & ~keep);
 }
 PSG_DEV uint64_t wave_transpose64(uint64_t r, int lane) {
   r = transpose_stage<32, 0x00000000FFFFFFFFull>(r, lane);
@@ -90,14 +159,19 @@ PSG_DEV uint64_t wave_transpose64(uint64_t r, int lane) {
 template <int W>
 PSG_DEV void eps_check(Grp<W>& g, Checks& ck, int c, const Mask<W>& full, bool decided, double decision, double eps,
                        bool anyI, double lo, double hi, bool pred) {
-  const bool nanD = g.any(decided && decision != decision);
-  const bool ok = decided && decision == decision;
-  const bool anyD = g.any(ok);
-  const int64_t kd = total_key(decision);
-  const double mx = key_value(g.max64(kd, ok));
-  const double mn = key_value(g.min64(kd, ok));
-  const bool agree = !nanD && (!anyD || mx - mn <= eps);
-  const bool valid = !g.any(decided && !(anyI && lo <= decision && decision <= hi));
+  bool agree = true, valid = true;
+  if (g.any(decided)) {  // uniform: before the first decision both hold by definition
+    const bool nanD = g.any(decided && decision != decision);
+    const bool ok = decided && decision == decision;
+    const bool anyD = g.any(ok);
+    bool close = true;
+    if (anyD) {
+      const int64_t kd = total_key(decision);
+      close = key_value(g.max64(kd, ok)) - key_value(g.min64(kd, ok)) <= eps;
+    }
+    agree = !nanD && close;
+    valid = !g.any(decided && !(anyI && lo <= decision && decision <= hi));
+  }
   ck.record(fbit(agree, 0) | fbit(valid, 1) | fbit(pred, 2), meq(g.ballot(decided), full), c, g.lane);
 }
 
@@ -126,6 +200,14 @@ epsilon_kernel(KArgs a) {
   const Mask<W> full = mfull<W>(n);
   double* sx = L.sx[grp];
   int32_t* spid = L.spid[grp];
+  if constexpr (W == 1) {
+    for (uint32_t t = threadIdx.x; t < 256u * 8u; t += blockDim.x) {
+      uint32_t v = t >> 3, r = t & 7u;
+      for (; r > 0 && v != 0; --r) v &= v - 1u;  // drop r lowest set bits
+      L.sel8[t] = v ? (uint8_t)__builtin_ctz(v) : 0;
+    }
+    __syncthreads();
+  }
 
   InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
   for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
@@ -171,82 +253,79 @@ epsilon_kernel(KArgs a) {
         const Mask<W> U = mor(M, H);                             // V = mailbox ++ halted.values
         const int m = mpopc(U);
         pred = !g.any(!halted && m < n - f);
-        // sort every process's current x in total order (ties by pid): W = 1 a wave bitonic
-        // network over (key, pid) pairs, lane t ends with the t-th pair; W > 1 a rank count
-        // over the keys staged in LDS. Sorted values go to LDS (position = rank).
-        const int64_t key = total_key(x);
-        int32_t spid_r = 0;  // W = 1: pid at sorted position = lane
-        if constexpr (W == 1) {
-          int64_t skey = g.valid ? key : INT64_MAX;  // padding lanes sort last
-          spid_r = g.lane;
-          wave_sort_key_pid(skey, spid_r, g.lane);
-          const double xs = __shfl(x, spid_r);
-          if (g.lane < n) sx[g.lane] = xs;
-        } else {
-          L.keys[g.pid] = key;
-          __syncthreads();
-          int rank = 0;
-          for (int j = 0; j < n; ++j) {
-            const int64_t kj = L.keys[j];
-            rank += (kj < key || (kj == key && j < g.pid)) ? 1 : 0;
-          }
-          if (g.valid) {
-            sx[rank] = x;
-            spid[rank] = g.pid;
-          }
-        }
-        lds_sync<W>();
         // per lane: min, max, V(2f) and the trimmed every-2f-th sum over the members of
-        // its own V (Epsilon.scala:31-42)
+        // its own V (Epsilon.scala:31-42); no V is read in a round where every process that
+        // still runs decides (r > maxR), so that round skips the sort
         double first = 0.0, last = 0.0, e2f = 0.0, sum = 0.0;
         int cnt = 0;
-        if constexpr (W == 1) {
-          // Us = V as a mask over sorted positions (bit t: the process at position t is in
-          // V), from the sorted pid column read at uniform positions. The selected members
-          // j = f, 3f, 5f, ... < m - f are then found by dropping the lowest set bits, and
-          // only those positions are read from LDS.
-          // Us(p) bit t = [sorted position t's process is in U(p)]: transpose U (lane q: the
-          // receivers whose V holds q), fetch that column for position t's process, and
-          // transpose back (two bit-matrix transposes and one shuffle; padding processes
-          // sort last and are in no U)
-          const uint64_t Ut = wave_transpose64(U.w[0], g.lane);
-          const uint64_t Us = wave_transpose64((uint64_t)__shfl((unsigned long long)Ut, spid_r), g.lane);
-          if (!halted && m > 0) {
-            if (k == 0) {
-              first = sx[__builtin_ctzll(Us)];
-              last = sx[63 - __builtin_clzll(Us)];
-              if (m > 2 * f) {
-                uint64_t S = Us;
-                for (int d = 0; d < 2 * f; ++d) S &= S - 1;
-                e2f = sx[__builtin_ctzll(S)];
-              }
-            } else if (k <= maxR) {
-              uint64_t S = Us;
-              for (int d = 0; d < f; ++d) S &= S - 1;
-              for (int j = f; j < m - f; j += 2 * f) {  // ascending left fold from 0.0
-                sum += sx[__builtin_ctzll(S)];
-                ++cnt;
-                for (int d = 0; d < 2 * f; ++d) S &= S - 1;
-              }
+        if (g.any(!halted && k <= maxR)) {
+          // sort every process's current x in total order (ties by pid): W = 1 a wave bitonic
+          // network over (key, pid) pairs, lane t ends with the t-th pair; W > 1 a rank count
+          // over the keys staged in LDS. Sorted values go to LDS (position = rank).
+          const int64_t key = total_key(x);
+          int32_t spid_r = 0;  // W = 1: pid at sorted position = lane
+          if constexpr (W == 1) {
+            int64_t skey = g.valid ? key : INT64_MAX;  // padding lanes sort last
+            spid_r = g.lane;
+            wave_sort_key_pid(skey, spid_r, g.lane);
+            const double xs = __shfl(x, spid_r);
+            if (g.lane < n) sx[g.lane] = xs;
+          } else {
+            L.keys[g.pid] = key;
+            __syncthreads();
+            int rank = 0;
+            for (int j = 0; j < n; ++j) {
+              const int64_t kj = L.keys[j];
+              rank += (kj < key || (kj == key && j < g.pid)) ? 1 : 0;
+            }
+            if (g.valid) {
+              sx[rank] = x;
+              spid[rank] = g.pid;
             }
           }
-        } else {
-          // W > 1: every lane walks the sorted list once with broadcast LDS reads;
-          // the selected members are tracked with a running index (no modulo)
-          int j = 0, nsel = f;
-          const int jhi = m - f;
-          for (int t = 0; t < n; ++t) {
-            if (mtest(U, spid[t])) {
-              const double v = sx[t];
-              if (j == 0) first = v;
-              last = v;
-              if (j == 2 * f) e2f = v;
-              if (j == nsel && j < jhi) {
-                sum += v;
-                ++cnt;
-                nsel += 2 * f;
+          lds_sync<W>();
+          if constexpr (W == 1) {
+            // Us = V as a mask over sorted positions (bit t: the process at position t is in
+            // V), from the sorted pid column read at uniform positions. The selected members
+            // j = f, 3f, 5f, ... < m - f are then found by rank select (RankSel), and only
+            // those positions are read from LDS.
+            // Us(p) bit t = [sorted position t's process is in U(p)]: transpose U (lane q: the
+            // receivers whose V holds q), fetch that column for position t's process, and
+            // transpose back (two bit-matrix transposes and one shuffle; padding processes
+            // sort last and are in no U)
+            const uint64_t Ut = wave_transpose64(U.w[0], g.lane);
+            const uint64_t Us = wave_transpose64((uint64_t)__shfl((unsigned long long)Ut, spid_r), g.lane);
+            if (!halted && m > 0) {
+              const RankSel rs(Us);
+              if (k == 0) {
+                first = sx[__builtin_ctzll(Us)];
+                last = sx[63 - __builtin_clzll(Us)];
+                if (m > 2 * f) e2f = sx[rs.at((uint32_t)(2 * f), L.sel8)];
+              } else if (k <= maxR) {
+                for (int j = f; j < m - f; j += 2 * f) {  // ascending left fold from 0.0
+                  sum += sx[rs.at((uint32_t)j, L.sel8)];
+                  ++cnt;
+                }
               }
-              ++j;
+            }
+          } else {
+            // W > 1: every lane walks the sorted list once with broadcast LDS reads;
+            // the selected members are tracked with a running index (no modulo)
+            int j = 0, nsel = f;
+            const int jhi = m - f;
+            for (int t = 0; t < n; ++t) {
+              if (mtest(U, spid[t])) {
+                const double v = sx[t];
+                if (j == 0) first = v;
+                last = v;
+                if (j == 2 * f) e2f = v;
+                if (j == nsel && j < jhi) {
+                  sum += v;
+                  ++cnt;
+                  nsel += 2 * f;
+                }
+                ++j;
+              }
             }
           }
         }
