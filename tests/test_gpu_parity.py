@@ -303,6 +303,10 @@ EPS_CASES = [
         drop_log2=3, good_round=0.0, crash_fmax=4))),
     ("eps-mutant-n7", psync.EpsilonConsensus(1, 0.01, variant=1), 7, 3000, dict(seed=66, schedule=psync.HOSchedule(
         drop_log2=2, good_round=0.0, ho_min=5))),
+    # W = 1 rank select (RankSel) extremes: f = 1 selects every other member (~30 selects per
+    # lane per round, every byte of the position mask), f = 10 steps 20 positions at a time
+    ("eps-n64-f1", psync.EpsilonConsensus(1, 1e-9), 64, 500, dict(seed=69)),
+    ("eps-n64-f10", psync.EpsilonConsensus(10, 1e-4), 64, 500, dict(seed=71)),
     ("eps-n100-W2", psync.EpsilonConsensus(10, 1e-5), 100, 300, dict(seed=67, rounds=16)),
     ("eps-n256-W4", psync.EpsilonConsensus(40, 1e-3), 256, 60, dict(seed=68, rounds=16)),
 ]
