@@ -176,7 +176,7 @@ PSG_DEV void eps_check(Grp<W>& g, Checks& ck, int c, const Mask<W>& full, bool d
 }
 
 #ifndef PSG_EPS_WPE
-#define PSG_EPS_WPE 6  // W = 1 occupancy target: 6 is scratch-free (7 spilled 40 B: log()'s hoisted f64 constants); 14.23 vs 14.13 ms at 7 (W2 row, round-4 A/B)
+#define PSG_EPS_WPE 6  // W = 1 occupancy target (round 4: 14.23 vs 14.13 ms at 7); round 5: 96 B scratch at 6 (log()'s hoisted f64 constants, reloaded once per instance), 5 measured slower (12.17 vs 11.63 ms)
 #endif
 template <int W, bool XHO>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? PSG_EPS_WPE : 1)))
