@@ -266,6 +266,16 @@ def run_variant(rank, world, args, V, steps, warmup, devices=None):
     return {"summary": total, "dt": dt_max, "kernel_s": max(per_rank), "per_rank_kernel_s": per_rank, "cfg": cfg}
 
 
+def parallelism_label(mode, world, devices, instances):
+    """What ran, stated truthfully: RCCL is named only when a process group exists (torchrun
+    ranks, world size 1 included); a directly started single process has no collective."""
+    if mode == "device-list":
+        return f"one context over devices {devices} (psg_config.devices), {instances} instances each, no collective"
+    if mode == "ranks":
+        return f"instance-sharded x{world} ranks (RCCL all-reduce of counters)"
+    return "single process, no collective"
+
+
 def dry_run(mode, world, rank, args):
     """--dry-run: the ranks exist and can all-reduce (gloo), nothing touches a GPU."""
     if mode == "ranks":
@@ -318,10 +328,7 @@ def main(argv=None):
         # a 24-B summary per instance); process state stays on chip for all R rounds
         hbm_bytes = args.instances * (args.n * (4 + 4 + 1) + 24)
         hbm_gbs = hbm_bytes / head["kernel_s"] / 1e9
-        if devices:
-            par = f"one context over devices {devices} (psg_config.devices), {args.instances} instances each"
-        else:
-            par = f"instance-sharded x{world} ranks (RCCL all-reduce of counters)"
+        par = parallelism_label(mode, world, devices, args.instances)
         out = {
             "metric": "checked process-rounds/sec (node), OTR n=64 w/ invariants; % HBM peak",
             "value": value,

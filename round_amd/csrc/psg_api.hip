@@ -92,6 +92,9 @@ struct psg_ctx {
   uint64_t fetch_cap = 0;
   uint64_t last_count = 0;
   int grid_max = 0;  // resident blocks for the algorithm's kernel
+  // packed KSet (n > 64): state handed from the general-round kernel to the uniform-t tail
+  // kernel, per batch row a header word, 64 lane words and n decisions (psg_kset.hip)
+  uint64_t* d_hand = nullptr;
   std::string err;
   // multi-device context (cfg.n_devices > 0): one single-device context per listed
   // device; every call splits its range into contiguous slices, one per device
@@ -224,6 +227,11 @@ static KArgs make_args(const psg_ctx* c) {
   a.ho_min = f.sched.ho_min;
   a.self_bit = f.sched.self_bit;
   a.counters = c->d_counters;
+  if (c->d_hand) {
+    a.hand_hdr = c->d_hand;
+    a.hand_meta = c->d_hand + c->cap;
+    a.hand_dec = reinterpret_cast<int32_t*>(c->d_hand + c->cap * 65);
+  }
   if (c->ho_loaded) {
     a.ho_in = c->d_ho;
     a.crash_in = c->ho_has_crash ? c->d_crash : nullptr;
@@ -601,6 +609,8 @@ int psg_create(psg_ctx** out, const psg_config* cfg) {
   CK(hipMalloc(&c->d_dround, sizeof(uint8_t) * cells));
   CK(hipMalloc(&c->d_inst, sizeof(psg_instance_summary) * c->cap));
   CK(hipMalloc(&c->d_counters, sizeof(unsigned long long) * NCOUNTERS_ALLOC));
+  if (cfg->alg == PSG_ALG_KSET && c->W > 1)  // 520 + 4n bytes per batch row (psg_kset.hip hand-off)
+    CK(hipMalloc(&c->d_hand, sizeof(uint64_t) * 65 * c->cap + sizeof(int32_t) * cells));
   const void* kp = kernel_ptr(cfg->alg, c->W);
   int per_cu = 0;
   const int threads = c->W == 1 ? 256 : 64 * c->W;
@@ -1466,6 +1476,7 @@ void psg_destroy(psg_ctx* c) {
   if (c->d_dround) (void)hipFree(c->d_dround);
   if (c->d_inst) (void)hipFree(c->d_inst);
   if (c->d_counters) (void)hipFree(c->d_counters);
+  if (c->d_hand) (void)hipFree(c->d_hand);
   if (c->d_ids) (void)hipFree(c->d_ids);
   if (c->d_rec) (void)hipFree(c->d_rec);
   if (c->d_init_f64) (void)hipFree(c->d_init_f64);

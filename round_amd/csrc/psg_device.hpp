@@ -68,6 +68,12 @@ struct KArgs {
   const int32_t* crash_in;
   uint64_t ho_base;
   uint64_t init_base;  // fetch path with staged inputs: init row of id `inst` is inst - init_base
+  // packed KSet's hand-off from the general-round kernel to the uniform-t tail kernel
+  // (psg_kset.hip): per batch row a header word, 64 per-lane state words and the decisions of
+  // the processes halted before the hand-off ([row][n])
+  uint64_t* hand_hdr;
+  uint64_t* hand_meta;
+  int32_t* hand_dec;
 };
 
 // Initial value of process pid of batch element i (global id inst): staged rows
@@ -130,8 +136,9 @@ enum { C_FAIL = 0, C_DECIDED = PSG_MAX_CHECKS, C_DIGEST = PSG_MAX_CHECKS + 1,
        // (4 phase slots, then wave-lifetime s_memrealtime ticks summed, ~min start, max end, waves,
        // then (start, end) per wave for the first 16384 waves)
        // instance queues (InstanceQueue): NQUEUES counters, one per 128 B line
-       C_QUEUE = NCOUNTERS, NQUEUES = 8, QUEUE_STRIDE = 16,
-       C_TIMER = C_QUEUE + NQUEUES * QUEUE_STRIDE, NTIMERS = 8, NSTAMP_WAVES = 16384,
+       // (two regions: a launch's second kernel — packed KSet's uniform-t tail — takes its own)
+       C_QUEUE = NCOUNTERS, NQUEUES = 8, QUEUE_STRIDE = 16, NQUEUE_REGIONS = 2,
+       C_TIMER = C_QUEUE + NQUEUE_REGIONS * NQUEUES * QUEUE_STRIDE, NTIMERS = 8, NSTAMP_WAVES = 16384,
        T_RT_SUM = NTIMERS, T_RT_MIN = NTIMERS + 1, T_RT_MAX = NTIMERS + 2, T_WAVES = NTIMERS + 3,
        T_STAMPS = NTIMERS + 4,
        NTIMER_SLOTS = PSG_PHASE_TIMERS ? T_STAMPS + 2 * NSTAMP_WAVES : 0, NCOUNTERS_ALLOC = C_TIMER + NTIMER_SLOTS };
@@ -821,8 +828,9 @@ PSG_DEV void lds_sync() {
 #ifndef PSG_QUEUE_CHUNK
 #define PSG_QUEUE_CHUNK 4
 #endif
-template <int W>
+template <int W, int REGION = 0>
 struct InstanceQueue {
+  static_assert(REGION >= 0 && REGION < NQUEUE_REGIONS, "queue region");
   static constexpr uint64_t kChunk = W == 1 ? PSG_QUEUE_CHUNK : PSG_QUEUE_CHUNK_WIDE;
   static constexpr uint64_t kDone = ~0ull;
   uint64_t cur = 0, lim = 0;  // uniform: [cur, lim) is this group's current chunk
@@ -837,7 +845,7 @@ struct InstanceQueue {
       const int q = (home + tries) % NQUEUES;
       const uint64_t lo = a.count * q / NQUEUES, hi = a.count * (q + 1) / NQUEUES;
       if (lo >= hi) continue;
-      const uint64_t v = grab(&a.counters[C_QUEUE + q * QUEUE_STRIDE]);
+      const uint64_t v = grab(&a.counters[C_QUEUE + (REGION * NQUEUES + q) * QUEUE_STRIDE]);
       if (lo + v < hi) {
         cur = lo + v;
         lim = cur + kChunk < hi ? cur + kChunk : hi;

@@ -180,7 +180,14 @@ PSG_DEV void pk_and_or(const Mask<W>& a, const Mask<W>& o, Mask<W>& all, Mask<W>
   }
 }
 
-template <int W>
+// Hand-off to the uniform-t tail kernel (HAND, below). Header word of batch row i: bits 0-7 the
+// round the tail resumes at, bit 8 its deciders' "pick(t) is not an initial value", bit 9 "the
+// instance was finished here", bits 32-63 pick(t) of the common t. Per-lane word: bits 0-7 the
+// lane's Checks::ffv, 8-19 the flag word fw (decider bits 0-3, not-initial bits 8-11), 32-63 the
+// slots' halt rounds as bytes (0xFF = not halted). Decisions of halted processes in [row][n].
+constexpr uint64_t kHandDone = 1ull << 9;
+
+template <int W, bool HAND>
 PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, KsPk<W>& L, KsStage<W>& S,
                          int sbuf, int32_t* x0lds, BlockCounters* bc, PhaseTimers& pt) {
   const int n = a.n, kk = a.param;
@@ -244,10 +251,32 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
   // closed form and the classes / columns are skipped: same = |M|, t unchanged.
   bool tuni = false;
   const bool lazy = sc.drop == 0 && sc.ho_min < 0;  // crash-round survival words drawn on demand (below)
+  // HAND: the rounds from the first with every alive t equal (or with every process halted) run
+  // in kset_tail_kernel, whose live state fits twice the waves per SIMD; this kernel stores the
+  // state that kernel needs and leaves the instance.
+  auto handoff = [&](int k, int32_t pu, uint32_t punot) {
+    uint32_t hr = 0;
+#pragma unroll
+    for (int j = 0; j < W; ++j) hr |= ((uint32_t)halt_round[j] & 0xFFu) << (8 * j);
+    const uint32_t x = ((uint32_t)ck.ffv & 0xFFu) | ((fw & 0xF0Fu) << 8);
+    a.hand_meta[i * 64 + (uint64_t)P.lane] = (uint64_t)x | ((uint64_t)hr << 32);
+#pragma unroll
+    for (int j = 0; j < W; ++j)
+      if (P.val[j] && halt_round[j] >= 0) a.hand_dec[i * (uint64_t)a.n + (uint64_t)P.pid(j)] = decision[j];
+    if (P.lane == 0) a.hand_hdr[i] = (uint64_t)((uint32_t)k | (punot << 8)) | ((uint64_t)(uint32_t)pu << 32);
+    lds_sync<1>();  // x0s reads done before the next instance restages them
+    pt.mark(3);
+  };
   for (int k = 0; k < a.R; ++k) {
     // Once every process halted the state is frozen; the round has no step to take, but its
     // check point is still evaluated (every counted process-round is checked).
     const bool live = many(act);
+    if constexpr (HAND) {
+      if (!live) {
+        handoff(k, 0, 0u);
+        return;
+      }
+    }
     if (live) {
       Mask<W> goodS;
       const bool good = sc.good_round(k, P.lane, a.R, goodS);
@@ -292,6 +321,13 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
 #pragma unroll
         for (int j = 0; j < W; ++j) dif |= (uint32_t)((act.w[j] >> P.lane) & 1ull) & (meq(t[j], t0) ? 0u : 1u);
         tuni = !pk_any(dif);
+        if constexpr (HAND) {
+          if (tuni) {  // every decision from here on is pick(t0); its X0 probe taken once
+            const int32_t pu = kset_pick<W>(t0, L.x0s, Emin, xmin);
+            handoff(k, pu, 1u - X0.contains01(pu));
+            return;
+          }
+        }
       }
       // the pre-round t masks staged for the class reads and adoptions ([word][pid])
       const bool staged = !tuni && (!closed || many(Dm));
@@ -388,7 +424,7 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
       pt.add(6, cols && !colform ? mpopc(rem) : 0);
       pt.add(7, many(CN));
       // one slot at a time (its HO set M, its merge or adoption)
-      if (tuni) {
+      if (!HAND && tuni) {
         // Every sender's t is t_p, so a step reads its mailbox only through hc (some decider
         // heard) and same = |M| > need (KSetAgreement.scala:46-58), and t never changes (a
         // union or an adoption is t_p again). In a crash round (no benign loss, no ho_min) M
@@ -531,14 +567,193 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
 #pragma unroll
   for (int j = 0; j < W; ++j) mainx[j] = P.val[j] ? kset_pick<W>(t[j], L.x0s, Emin, xmin) : 0;
   pk_finish<W>(P, a, i, ck, 2, decision, halt_round, halt_round, mainx, bc);
+  if constexpr (HAND) {
+    if (P.lane == 0) a.hand_hdr[i] = kHandDone;
+  }
   lds_sync<1>();  // x0s reads done before the next instance restages them
+  pt.mark(3);
+}
+
+// The uniform-t tail of a handed-off instance (kset_packed<W, true>): every alive process holds
+// the same t (or none is alive), so no round changes any t (a union of equal t's and an adoption
+// are that t), every decision is pick(t) = pu, and a step reads its mailbox only through hc (some
+// decider heard) and |M| > n - k (KSetAgreement.scala:46-58). The lane keeps its slots' decision,
+// halt round and crash round and one flag word — no t masks, staging, classes, columns or X0 set —
+// so the kernel runs at twice the general kernel's waves per SIMD. Every check point is evaluated.
+template <int W, bool LAZY>
+PSG_DEV void kset_tail(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, uint64_t h, BlockCounters* bc,
+                       PhaseTimers& pt) {
+  const int n = a.n, kk = a.param;
+  const int need = a.variant == 1 ? 1 : n - kk;  // same.size > n - k (KSetAgreement.scala:56)
+  const int k0 = (int)(h & 0xFFu);
+  const uint32_t punot = (uint32_t)(h >> 8) & 1u;
+  const int32_t pu = (int32_t)(uint32_t)(h >> 32);
+  Sched<W, false> sc;
+  sc.setup(a, inst, P.lane, false);
+  sc.prep_good(k0, P.lane, a.R);
+  // Per-slot state packed so that the slot loop runs rolled (one copy of its Philox draws, no
+  // per-slot arrays indexed by the loop variable): halt rounds and crash rounds as bytes of one
+  // word each (0xFF = none), decider / not-initial bits in fw; a slot's decision is its loaded
+  // one if it halted before the hand-off (hb), else pu.
+  uint32_t crp = ~0u;
+  if (a.crash_fmax >= 0) {
+    const uint64_t w0 = rword(a.seed, inst, ROUND_CRASH, PID_GLOBAL, 0);
+    const uint64_t w1 = rword(a.seed, inst, ROUND_CRASH, PID_GLOBAL, 1);
+#pragma unroll 1
+    for (int j = 0; j < W; ++j) {
+      const int32_t c = P.pid(j) < n ? Sched<W>::crash_of(a, inst, (uint32_t)P.pid(j), w0, w1) : -1;
+      crp &= ~((~(uint32_t)c & 0xFFu) << (8 * j));
+    }
+  }
+  const uint64_t m = a.hand_meta[i * 64 + (uint64_t)P.lane];
+  Checks ck;
+  ck.ffv = (int32_t)(m & 0xFFu);
+  uint32_t fw = ((uint32_t)m >> 8) & 0xF0Fu;
+  uint32_t hr = (uint32_t)(m >> 32);
+  int32_t decl[W];
+  uint32_t hb = 0, al[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    const bool halted = ((hr >> (8 * j)) & 0xFFu) != 0xFFu;
+    decl[j] = 0;
+    if (P.val[j] && halted) decl[j] = a.hand_dec[i * (uint64_t)n + (uint64_t)P.pid(j)];
+    hb |= (halted ? 1u : 0u) << j;
+    al[j] = P.val[j] & (halted ? 0u : 1u);
+  }
+  Mask<W> act = P.ballot(al);
+  auto check = [&](int c) {
+    uint32_t decided[W], notinit[W];
+    int32_t decision[W], cr[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      decided[j] = ((hr >> (8 * j)) & 0xFFu) != 0xFFu ? 1u : 0u;
+      notinit[j] = (fw >> (8 + j)) & 1u;
+      decision[j] = ((hb >> j) & 1u) ? decl[j] : pu;
+      cr[j] = ((crp >> (8 * j)) & 0xFFu) == 0xFFu ? -1 : (int32_t)((crp >> (8 * j)) & 0xFFu);
+    }
+    pk_kagree_check_m<W>(P, ck, c, kk, decided, decision, cr, notinit);
+  };
+  pt.mark(0);
+  for (int k = k0; k < a.R; ++k) {
+    const bool live = many(act);
+    if (live) {
+      Mask<W> goodS;
+      const bool good = sc.good_round(k, P.lane, a.R, goodS);
+      Mask<W> CB = mzero<W>(), CN = mzero<W>();
+      if (sc.crash_on) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          const uint32_t c = (crp >> (8 * j)) & 0xFFu;  // 0xFF: correct
+          CB.w[j] = __builtin_amdgcn_ballot_w64(c < (uint32_t)k);
+          CN.w[j] = __builtin_amdgcn_ballot_w64(c == (uint32_t)k);
+        }
+      }
+      uint32_t dw[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) dw[j] = (fw >> j) & 1u;
+      const Mask<W> Dm = mand(P.ballot(dw), act);  // senders' decider flags (pre-state)
+      if constexpr (LAZY) {
+        // No benign loss and no ho_min (the C4 schedules): HO(p) = B0 \ CB \ (CN \ survivors_p),
+        // plus p itself under the runtime's self delivery (Sched::assemble). Ulo (every crashing
+        // sender lost) is uniform; so is, outside crash rounds, the whole mailbox. In a crash
+        // round M lies between Ulo and Uhi = Ulo + CNa: when both bounds give the same hc and
+        // |M| > need for every live slot of the wave, the round's survival words change nothing
+        // and are not drawn (each is a pure function of (instance, round, pid): skipping one moves
+        // no other draw); otherwise the slot draws the survival words of the crashing senders'
+        // 64-pid words only (Sched::draw's loss-free crash-round calls).
+        const Mask<W> B0 = good ? goodS : sc.full;
+        const Mask<W> Ulo = mand(mandn(B0, mor(CB, CN)), act);
+        const Mask<W> CNa = mand(mand(B0, CN), act);
+        const bool crashr = many(CNa);
+        const int plo_u = mpopc(Ulo), phi_u = plo_u + mpopc(CNa);
+        const bool hlo_u = many(mand(Ulo, Dm)), hhi_u = hlo_u || many(mand(CNa, Dm));
+        uint32_t cw = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) cw |= CNa.w[w] ? 1u << w : 0u;
+#pragma unroll 1
+        for (int j = 0; j < W; ++j) {
+          const int pid = P.pid(j);
+          const uint32_t sh = 8u * (uint32_t)j;
+          const bool halted = ((hr >> sh) & 0xFFu) != 0xFFu;
+          const uint32_t decider = (fw >> j) & 1u;
+          const uint32_t live_j = (pid < n ? 1u : 0u) & (halted ? 0u : 1u) & (1u - decider);
+          const bool self = sc.self_bit && mtest(act, pid);
+          const bool sd = self && mtest(Dm, pid);
+          const uint32_t hlo = (hlo_u || sd) ? 1u : 0u;
+          const uint32_t plo = plo_u + ((self && !mtest(Ulo, pid)) ? 1 : 0) > need ? 1u : 0u;
+          uint32_t hc = hlo, big = plo;
+          if (crashr) {
+            const uint32_t hhi = (hhi_u || sd) ? 1u : 0u;
+            const uint32_t phi = phi_u + ((self && !mtest(Ulo, pid) && !mtest(CNa, pid)) ? 1 : 0) > need ? 1u : 0u;
+            // undetermined: hc open, or no decider heard for sure and |M| > need open
+            if (pk_any(live_j & ((hlo ^ hhi) | ((1u - hlo) & (plo ^ phi))))) {
+              Mask<W> S = mzero<W>();  // the crashing senders p hears
+#pragma unroll
+              for (int c2 = 0; 2 * c2 < W; ++c2) {
+                if (!((cw >> (2 * c2)) & 3u)) continue;
+                const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), (uint32_t)k,
+                                      (uint32_t)pid + ((uint32_t)c2 << 16), (uint32_t)a.seed,
+                                      (uint32_t)(a.seed >> 32));
+                S.w[2 * c2] = CNa.w[2 * c2] & ((uint64_t)o.x | ((uint64_t)o.y << 32));
+                if (2 * c2 + 1 < W) S.w[2 * c2 + 1] = CNa.w[2 * c2 + 1] & ((uint64_t)o.z | ((uint64_t)o.w << 32));
+              }
+              const Mask<W> M = mor(Ulo, S);
+              hc = (many(mand(M, Dm)) || sd) ? 1u : 0u;
+              big = mpopc(M) + ((self && !mtest(M, pid)) ? 1 : 0) > need ? 1u : 0u;
+            }
+          }
+          if (!halted && decider) {  // decide(pick(t)) = pu; exitAtEndOfRound (KSetAgreement.scala:48-50)
+            hr = (hr & ~(0xFFu << sh)) | ((uint32_t)k << sh);
+            fw |= punot << (8 + j);
+          }
+          fw |= (live_j & (hc | big)) << j;  // adopts, or merges with same > n - k: decider
+        }
+      } else {  // the general schedule: each slot's HO set drawn in full
+#pragma unroll 1
+        for (int j = 0; j < W; ++j) {
+          const int pid = P.pid(j);
+          const uint32_t sh = 8u * (uint32_t)j;
+          const bool halted = ((hr >> sh) & 0xFFu) != 0xFFu;
+          const uint32_t decider = (fw >> j) & 1u;
+          const uint32_t live_j = (pid < n ? 1u : 0u) & (halted ? 0u : 1u) & (1u - decider);
+          const Mask<W> M = mand(sc.ho(k, pid, good, goodS, CB, CN), act);
+          const uint32_t hc = many(mand(M, Dm)) ? 1u : 0u;
+          const uint32_t big = mpopc(M) > need ? 1u : 0u;
+          if (!halted && decider) {  // decide(pick(t)) = pu; exitAtEndOfRound (KSetAgreement.scala:48-50)
+            hr = (hr & ~(0xFFu << sh)) | ((uint32_t)k << sh);
+            fw |= punot << (8 + j);
+          }
+          fw |= (live_j & (hc | big)) << j;  // adopts, or merges with same > n - k: decider
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < W; ++j) al[j] = P.val[j] & (((hr >> (8 * j)) & 0xFFu) != 0xFFu ? 0u : 1u);
+      act = P.ballot(al);
+    }
+    check(k + 1);
+    pt.mark(live ? 4 : 5);
+  }
+  // final x = pick(t): a process halted before the hand-off decided pick of its own (frozen) t,
+  // every other process holds the common t
+  int32_t decision[W], halt_round[W], mainx[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    const uint32_t b = (hr >> (8 * j)) & 0xFFu;
+    halt_round[j] = b == 0xFFu ? -1 : (int32_t)b;
+    decision[j] = b == 0xFFu ? 0 : (((hb >> j) & 1u) ? decl[j] : pu);
+    mainx[j] = ((hb >> j) & 1u) ? decl[j] : pu;
+  }
+  pk_finish<W>(P, a, i, ck, 2, decision, halt_round, halt_round, mainx, bc);
   pt.mark(3);
 }
 
 #ifndef PSG_KSET_PK_WPE
 #define PSG_KSET_PK_WPE 3  // W = 4: four 256-bit t masks per lane; 2 -> 3 after the per-slot state diet: C4 f=1 2.80 -> 2.18 ms
 #endif
-template <int W>
+#ifndef PSG_KSET_SPLIT
+#define PSG_KSET_SPLIT 1  // 1: general rounds here, the uniform-t tail in kset_tail_kernel; 0: one kernel
+#endif
+template <int W, bool HAND>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_KSET_PK_WPE))) kset_packed_kernel(KArgs a) {
   __shared__ BlockCounters bc;
   __shared__ KsPk<W> L[4];
@@ -555,7 +770,31 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_KS
   InstanceQueue<1> Q;
   for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
-    kset_packed<W>(P, a, i, inst, L[grp], S, grp * KsStage<W>::kBufs / 4, x0tab[grp], &bc, pt);
+    kset_packed<W, HAND>(P, a, i, inst, L[grp], S, grp * KsStage<W>::kBufs / 4, x0tab[grp], &bc, pt);
+  }
+  pt.flush(a.counters, P.lane);
+  __syncthreads();
+  counters_flush(&bc, a.counters, 2, a.R);
+}
+
+#ifndef PSG_KSET_TAIL_WPE
+#define PSG_KSET_TAIL_WPE 6  // waves/SIMD of the uniform-t tail kernel
+#endif
+template <int W, bool LAZY>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LAZY ? PSG_KSET_TAIL_WPE : 4))) kset_tail_kernel(KArgs a) {
+  __shared__ BlockCounters bc;
+  counters_init(&bc);
+  __syncthreads();
+  Pk<W> P;
+  P.setup(a.n);
+  PhaseTimers pt;  // profiling builds only: t0 setup, t3 finish, t4 check after a live round, t5 frozen round
+  pt.start();
+  InstanceQueue<1, 1> Q;  // the second queue region (the general kernel drained the first)
+  for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
+    const uint64_t h = a.hand_hdr[i];
+    if (h & kHandDone) continue;  // finished by the general kernel
+    const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
+    kset_tail<W, LAZY>(P, a, i, inst, h, &bc, pt);
   }
   pt.flush(a.counters, P.lane);
   __syncthreads();
@@ -736,8 +975,20 @@ template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
   if constexpr (W > 1) {  // seeded schedule, built-in checker: lane-packed path
     if (!a.ho_in && !a.trace) {
-      const int pg = pk_grid<PSG_ALG_KSET, W>((const void*)kset_packed_kernel<W>, a.count);
-      hipLaunchKernelGGL((kset_packed_kernel<W>), dim3(pg), dim3(256), 0, s, a);
+      if (PSG_KSET_SPLIT && a.hand_hdr) {  // general rounds, then the uniform-t tail (same stream)
+        const int pg = pk_grid<PSG_ALG_KSET, W>((const void*)kset_packed_kernel<W, true>, a.count);
+        hipLaunchKernelGGL((kset_packed_kernel<W, true>), dim3(pg), dim3(256), 0, s, a);
+        if (a.drop_log2 == 0 && a.ho_min < 0) {  // loss-free schedules: uniform mailboxes but crash rounds
+          const int tg = pk_grid<PSG_ALG_KSET | 0x100, W>((const void*)kset_tail_kernel<W, true>, a.count);
+          hipLaunchKernelGGL((kset_tail_kernel<W, true>), dim3(tg), dim3(256), 0, s, a);
+        } else {
+          const int tg = pk_grid<PSG_ALG_KSET | 0x300, W>((const void*)kset_tail_kernel<W, false>, a.count);
+          hipLaunchKernelGGL((kset_tail_kernel<W, false>), dim3(tg), dim3(256), 0, s, a);
+        }
+        return hipGetLastError();
+      }
+      const int pg = pk_grid<PSG_ALG_KSET | 0x200, W>((const void*)kset_packed_kernel<W, false>, a.count);
+      hipLaunchKernelGGL((kset_packed_kernel<W, false>), dim3(pg), dim3(256), 0, s, a);
       return hipGetLastError();
     }
   }

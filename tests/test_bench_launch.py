@@ -84,3 +84,14 @@ def test_bench_configs_gpus_two_spawns_two_ranks():
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     assert json.loads(lines[0]) == {"dry_run": True, "mode": "ranks", "world": 2, "ranks_seen": 2, "n_gpus": 2}
+
+
+def test_parallelism_label_states_whether_rccl_ran():
+    """The N = 1 line started directly has no process group: its label must not claim RCCL
+    (VERDICT r5 #7); under torchrun (world 1 included) the counters go through RCCL."""
+    single = bench.parallelism_label("single", 1, None, 10)
+    assert "RCCL" not in single and "no collective" in single
+    assert "RCCL" in bench.parallelism_label("ranks", 1, None, 10)
+    assert "x8 ranks" in bench.parallelism_label("ranks", 8, None, 10)
+    dl = bench.parallelism_label("device-list", 1, [0, 1], 10)
+    assert "RCCL" not in dl and "[0, 1]" in dl

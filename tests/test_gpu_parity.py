@@ -26,6 +26,9 @@ CASES = [
     ("otr-mutant-n8", psync.OTR(variant=1), 8, 3000, dict(schedule=H(drop_log2=1, good_round=0.0), seed=8)),
     ("otr-pureho", psync.OTR(), 12, 2000, dict(schedule=H(drop_log2=2, self_bit=False), seed=9)),
     ("otr-crash", psync.OTR(), 64, 500, dict(schedule=H(drop_log2=3, crash_fmax=20), seed=10)),
+    # at most 0 crashes: the library passes "no crash schedule" to the kernels (psg_api.hip make_args)
+    ("otr-crash-f0", psync.OTR(), 64, 1000, dict(schedule=H(drop_log2=3, crash_fmax=0), seed=30)),
+    ("lv-n64-f0", psync.LastVoting(), 64, 1000, dict(seed=31, schedule=H(drop_log2=3, crash_fmax=0))),
     ("lv-n64-crash", psync.LastVoting(), 64, 2000, dict(seed=11)),
     ("lv-n64-minpid", psync.LastVoting(), 64, 1000, dict(seed=12, tiebreak=abi.PSG_TIE_MIN_PID)),
     ("lv-n5", psync.LastVoting(), 5, 3000, dict(seed=13, value_range=4)),
@@ -61,6 +64,18 @@ CASES = [
                                                                                       crash_fmax=3))),
     ("kset-n192-mutant", psync.KSetAgreement(2, variant=1), 192, 100, dict(seed=84)),
     ("kset-n256-k2-V3", psync.KSetAgreement(2), 256, 100, dict(seed=85, value_range=3)),
+    # the uniform-t tail kernel (round 6): loss-free crash schedules (its uniform-mailbox form),
+    # pure HO, good rounds, at most 0 crashes, and ho_min (the general form)
+    ("kset-n256-f64-lossfree", psync.KSetAgreement(2), 256, 200, dict(seed=86, schedule=H(
+        drop_log2=0, good_round=0.0, crash_fmax=64))),
+    ("kset-n130-lossfree-pureho", psync.KSetAgreement(2), 130, 300, dict(seed=87, schedule=H(
+        drop_log2=0, good_round=0.0, crash_fmax=20, self_bit=False))),
+    ("kset-n200-lossfree-good", psync.KSetAgreement(3), 200, 200, dict(seed=88, value_range=4, schedule=H(
+        drop_log2=0, good_round=0.3, crash_fmax=30))),
+    ("kset-n256-f0", psync.KSetAgreement(2), 256, 200, dict(seed=89, schedule=H(drop_log2=0, good_round=0.0,
+                                                                                 crash_fmax=0))),
+    ("kset-n160-homin", psync.KSetAgreement(2), 160, 150, dict(seed=95, schedule=H(
+        drop_log2=3, good_round=0.1, crash_fmax=12, ho_min=120))),
     ("benor-n128", psync.BenOr(), 128, 300, dict(seed=25)),
     ("benor-n4", psync.BenOr(), 4, 3000, dict(seed=26)),
     ("benor-n64-mutant", psync.BenOr(variant=1), 64, 500, dict(seed=27)),

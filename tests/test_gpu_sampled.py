@@ -66,7 +66,7 @@ def test_c3_lastvoting_shard_boundaries(oracle_mod):
         _check(gr, ids, oracle_mod)
 
 
-@pytest.mark.parametrize("f", [8, 64])
+@pytest.mark.parametrize("f", [0, 8, 64])
 def test_c4_floodmin_f(f, oracle_mod):
     rng = random.Random(40 + f)
     ids = _ids(rng, 1_000_000, 40, extra=HIGH[:6])
@@ -74,10 +74,10 @@ def test_c4_floodmin_f(f, oracle_mod):
         _check(gr, ids, oracle_mod)
 
 
-@pytest.mark.parametrize("f", [1, 8, 32, 64])
+@pytest.mark.parametrize("f", [0, 1, 8, 32, 64])
 def test_c4_kset_f(f, oracle_mod):
-    """C4 KSet n=256 k=2 crash-stop sweep (bench_configs.py C4_kset_n256_k2_f*): the default
-    f < k, two inner points and the f = 64 end."""
+    """C4 KSet n=256 k=2 crash-stop sweep (bench_configs.py C4_kset_n256_k2_f*): f = 0 (no crash
+    schedule at all, psg_api.hip make_args), the default f < k, two inner points and the f = 64 end."""
     rng = random.Random(50 + f)
     ids = _ids(rng, 200_000, 24, extra=HIGH[:4])
     sched = psync.HOSchedule(drop_log2=0, good_round=0.0, crash_fmax=f)
