@@ -336,8 +336,11 @@ int psg_spec_compile_native(const char* text, int32_t alg, int32_t fused, int32_
  * against the Spec as written under any evaluator (tests). Same buffer contract as
  * psg_spec_native_source. Generator options for all three entry points (comma-separated:
  * nosym, nosplit, D<NAME>=<VALUE>) come from psg_spec_set_options on the calling thread, else
- * from the environment variable PSG_SPEC_OPTIONS; an unknown option, or a define naming a
- * probe-build switch (PSG_AB*), makes the entry point return PSG_EINVAL. */
+ * from the environment variable PSG_SPEC_OPTIONS; an unknown option, a define outside the
+ * generator knobs (PSG_PHASE_TIMERS, the PSG_*_WPE occupancy targets and the exact-alternative
+ * switches PSG_PHILOX_OPAQUE_KEYS, PSG_PHILOX_MAD64, PSG_XSHFL_MASK, PSG_QUEUE_CHUNK[_WIDE],
+ * PSG_MAJ_BITVOTE, PSG_BO_FLAGS_DPP) or a non-integer value makes the entry point return
+ * PSG_EINVAL. */
 int psg_spec_rewrite_text(const char* text, int32_t alg, char* out, size_t* out_len, char* err, size_t err_len);
 /* The HIP source psg_spec_compile_native compiles for these arguments (tests, inspection):
  * *src_len = capacity in, the size needed (with the terminating NUL) out; PSG_ERANGE when

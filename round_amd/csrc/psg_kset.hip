@@ -146,13 +146,17 @@ struct KsPk {
 #endif
 template <int W>
 struct KsStage {
+  static constexpr int kWaves = 4;  // kset_packed_kernel: 256-thread blocks, one instance per wave
   static constexpr int kBufs = PSG_KSET_STAGE_BUFS;
+  static_assert(kBufs >= 1 && kWaves % kBufs == 0, "every staging buffer is shared by the same number of waves");
   uint64_t ts[kBufs][64 * W * W];
   int lock[kBufs];
   PSG_DEV void init() {
     if (threadIdx.x < kBufs) lock[threadIdx.x] = 0;
   }
-  // wave-uniform; no wave holding a buffer ever waits for another wave, so every waiter gets it
+  // Wave-uniform spin lock. Deadlock-free because no wave holding a buffer ever waits for another
+  // wave: between acquire() and release() only wave-level syncs (lds_sync<1>) may run — a block
+  // barrier (__syncthreads) there would wait for a wave spinning here, which never arrives.
   PSG_DEV uint64_t* acquire(int b, int lane) {
     while (true) {
       int got = 0;
@@ -580,6 +584,9 @@ PSG_DEV void kset_packed(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t in
 // decider heard) and |M| > n - k (KSetAgreement.scala:46-58). The lane keeps its slots' decision,
 // halt round and crash round and one flag word — no t masks, staging, classes, columns or X0 set —
 // so the kernel runs at twice the general kernel's waves per SIMD. Every check point is evaluated.
+// LAZY (no benign loss, no ho_min: the C4 schedules): HO(p) = B0 \ CB \ (CN \ survivors_p), plus
+// p itself under the runtime's self delivery (Sched::assemble), so the mailboxes are uniform but
+// for the self bit and, in a crash round, the crashing senders p hears.
 template <int W, bool LAZY>
 PSG_DEV void kset_tail(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst, uint64_t h, BlockCounters* bc,
                        PhaseTimers& pt) {
@@ -591,45 +598,32 @@ PSG_DEV void kset_tail(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst
   Sched<W, false> sc;
   sc.setup(a, inst, P.lane, false);
   sc.prep_good(k0, P.lane, a.R);
-  // Per-slot state packed so that the slot loop runs rolled (one copy of its Philox draws, no
-  // per-slot arrays indexed by the loop variable): halt rounds and crash rounds as bytes of one
-  // word each (0xFF = none), decider / not-initial bits in fw; a slot's decision is its loaded
-  // one if it halted before the hand-off (hb), else pu.
-  uint32_t crp = ~0u;
-  if (a.crash_fmax >= 0) {
-    const uint64_t w0 = rword(a.seed, inst, ROUND_CRASH, PID_GLOBAL, 0);
-    const uint64_t w1 = rword(a.seed, inst, ROUND_CRASH, PID_GLOBAL, 1);
-#pragma unroll 1
-    for (int j = 0; j < W; ++j) {
-      const int32_t c = P.pid(j) < n ? Sched<W>::crash_of(a, inst, (uint32_t)P.pid(j), w0, w1) : -1;
-      crp &= ~((~(uint32_t)c & 0xFFu) << (8 * j));
-    }
-  }
+  int32_t cr[W];
+  pk_crash_rounds<W>(P, a, inst, cr);
   const uint64_t m = a.hand_meta[i * 64 + (uint64_t)P.lane];
   Checks ck;
   ck.ffv = (int32_t)(m & 0xFFu);
-  uint32_t fw = ((uint32_t)m >> 8) & 0xF0Fu;
-  uint32_t hr = (uint32_t)(m >> 32);
-  int32_t decl[W];
-  uint32_t hb = 0, al[W];
+  uint32_t fw = ((uint32_t)m >> 8) & 0xF0Fu;  // decider bit j, not-initial bit 8 + j
+  int32_t decision[W], halt_round[W], mainx[W];
+  uint32_t al[W];
 #pragma unroll
   for (int j = 0; j < W; ++j) {
-    const bool halted = ((hr >> (8 * j)) & 0xFFu) != 0xFFu;
-    decl[j] = 0;
-    if (P.val[j] && halted) decl[j] = a.hand_dec[i * (uint64_t)n + (uint64_t)P.pid(j)];
-    hb |= (halted ? 1u : 0u) << j;
-    al[j] = P.val[j] & (halted ? 0u : 1u);
+    const uint32_t b = (uint32_t)(m >> (32 + 8 * j)) & 0xFFu;
+    halt_round[j] = b == 0xFFu ? -1 : (int32_t)b;
+    decision[j] = 0;
+    if (P.val[j] && halt_round[j] >= 0) decision[j] = a.hand_dec[i * (uint64_t)n + (uint64_t)P.pid(j)];
+    // final x = pick(t): a process halted before the hand-off decided pick of its own (frozen) t,
+    // every other process holds the common t
+    mainx[j] = halt_round[j] >= 0 ? decision[j] : pu;
+    al[j] = P.val[j] & (halt_round[j] >= 0 ? 0u : 1u);
   }
   Mask<W> act = P.ballot(al);
   auto check = [&](int c) {
     uint32_t decided[W], notinit[W];
-    int32_t decision[W], cr[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) {
-      decided[j] = ((hr >> (8 * j)) & 0xFFu) != 0xFFu ? 1u : 0u;
+      decided[j] = halt_round[j] >= 0 ? 1u : 0u;
       notinit[j] = (fw >> (8 + j)) & 1u;
-      decision[j] = ((hb >> j) & 1u) ? decl[j] : pu;
-      cr[j] = ((crp >> (8 * j)) & 0xFFu) == 0xFFu ? -1 : (int32_t)((crp >> (8 * j)) & 0xFFu);
     }
     pk_kagree_check_m<W>(P, ck, c, kk, decided, decision, cr, notinit);
   };
@@ -643,105 +637,98 @@ PSG_DEV void kset_tail(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst
       if (sc.crash_on) {
 #pragma unroll
         for (int j = 0; j < W; ++j) {
-          const uint32_t c = (crp >> (8 * j)) & 0xFFu;  // 0xFF: correct
-          CB.w[j] = __builtin_amdgcn_ballot_w64(c < (uint32_t)k);
-          CN.w[j] = __builtin_amdgcn_ballot_w64(c == (uint32_t)k);
+          CB.w[j] = __builtin_amdgcn_ballot_w64((uint32_t)cr[j] < (uint32_t)k);
+          CN.w[j] = __builtin_amdgcn_ballot_w64(cr[j] == k);
         }
       }
       uint32_t dw[W];
 #pragma unroll
       for (int j = 0; j < W; ++j) dw[j] = (fw >> j) & 1u;
       const Mask<W> Dm = mand(P.ballot(dw), act);  // senders' decider flags (pre-state)
+      uint32_t hcb = 0, bigb = 0;                   // per slot j: hc (some decider heard), |M| > need
       if constexpr (LAZY) {
-        // No benign loss and no ho_min (the C4 schedules): HO(p) = B0 \ CB \ (CN \ survivors_p),
-        // plus p itself under the runtime's self delivery (Sched::assemble). Ulo (every crashing
-        // sender lost) is uniform; so is, outside crash rounds, the whole mailbox. In a crash
-        // round M lies between Ulo and Uhi = Ulo + CNa: when both bounds give the same hc and
-        // |M| > need for every live slot of the wave, the round's survival words change nothing
-        // and are not drawn (each is a pure function of (instance, round, pid): skipping one moves
-        // no other draw); otherwise the slot draws the survival words of the crashing senders'
-        // 64-pid words only (Sched::draw's loss-free crash-round calls).
+        // Ulo (every crashing sender lost) is uniform. In a crash round M lies between Ulo and
+        // Uhi = Ulo + CNa: when both bounds give the same hc and |M| > need for every live slot
+        // of the wave, the round's survival words change nothing and are not drawn (each is a pure
+        // function of (instance, round, pid): skipping one moves no other draw); otherwise the
+        // slot draws the survival words of the crashing senders' 64-pid words only (Sched::draw's
+        // loss-free crash-round calls).
         const Mask<W> B0 = good ? goodS : sc.full;
         const Mask<W> Ulo = mand(mandn(B0, mor(CB, CN)), act);
         const Mask<W> CNa = mand(mand(B0, CN), act);
         const bool crashr = many(CNa);
         const int plo_u = mpopc(Ulo), phi_u = plo_u + mpopc(CNa);
         const bool hlo_u = many(mand(Ulo, Dm)), hhi_u = hlo_u || many(mand(CNa, Dm));
-        uint32_t cw = 0;
+        const uint32_t selfb = sc.self_bit ? 1u : 0u;
+        uint32_t und = 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w) cw |= CNa.w[w] ? 1u << w : 0u;
-#pragma unroll 1
         for (int j = 0; j < W; ++j) {
-          const int pid = P.pid(j);
-          const uint32_t sh = 8u * (uint32_t)j;
-          const bool halted = ((hr >> sh) & 0xFFu) != 0xFFu;
-          const uint32_t decider = (fw >> j) & 1u;
-          const uint32_t live_j = (pid < n ? 1u : 0u) & (halted ? 0u : 1u) & (1u - decider);
-          const bool self = sc.self_bit && mtest(act, pid);
-          const bool sd = self && mtest(Dm, pid);
-          const uint32_t hlo = (hlo_u || sd) ? 1u : 0u;
-          const uint32_t plo = plo_u + ((self && !mtest(Ulo, pid)) ? 1 : 0) > need ? 1u : 0u;
-          uint32_t hc = hlo, big = plo;
+          const uint32_t live_j = P.val[j] & (halt_round[j] >= 0 ? 0u : 1u) & (1u - ((fw >> j) & 1u));
+          const uint32_t self = selfb & (uint32_t)(act.w[j] >> P.lane) & 1u;
+          const uint32_t sd = self & (uint32_t)(Dm.w[j] >> P.lane);
+          const uint32_t inlo = (uint32_t)(Ulo.w[j] >> P.lane) & 1u;
+          const uint32_t hlo = (hlo_u ? 1u : 0u) | sd;
+          const uint32_t plo = plo_u + (int)(self & (1u - inlo)) > need ? 1u : 0u;
+          hcb |= hlo << j;
+          bigb |= plo << j;
           if (crashr) {
-            const uint32_t hhi = (hhi_u || sd) ? 1u : 0u;
-            const uint32_t phi = phi_u + ((self && !mtest(Ulo, pid) && !mtest(CNa, pid)) ? 1 : 0) > need ? 1u : 0u;
+            const uint32_t inhi = inlo | ((uint32_t)(CNa.w[j] >> P.lane) & 1u);
+            const uint32_t hhi = (hhi_u ? 1u : 0u) | sd;
+            const uint32_t phi = phi_u + (int)(self & (1u - inhi)) > need ? 1u : 0u;
             // undetermined: hc open, or no decider heard for sure and |M| > need open
-            if (pk_any(live_j & ((hlo ^ hhi) | ((1u - hlo) & (plo ^ phi))))) {
-              Mask<W> S = mzero<W>();  // the crashing senders p hears
-#pragma unroll
-              for (int c2 = 0; 2 * c2 < W; ++c2) {
-                if (!((cw >> (2 * c2)) & 3u)) continue;
-                const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), (uint32_t)k,
-                                      (uint32_t)pid + ((uint32_t)c2 << 16), (uint32_t)a.seed,
-                                      (uint32_t)(a.seed >> 32));
-                S.w[2 * c2] = CNa.w[2 * c2] & ((uint64_t)o.x | ((uint64_t)o.y << 32));
-                if (2 * c2 + 1 < W) S.w[2 * c2 + 1] = CNa.w[2 * c2 + 1] & ((uint64_t)o.z | ((uint64_t)o.w << 32));
-              }
-              const Mask<W> M = mor(Ulo, S);
-              hc = (many(mand(M, Dm)) || sd) ? 1u : 0u;
-              big = mpopc(M) + ((self && !mtest(M, pid)) ? 1 : 0) > need ? 1u : 0u;
-            }
+            und |= (live_j & ((hlo ^ hhi) | ((1u - hlo) & (plo ^ phi)))) << j;
           }
-          if (!halted && decider) {  // decide(pick(t)) = pu; exitAtEndOfRound (KSetAgreement.scala:48-50)
-            hr = (hr & ~(0xFFu << sh)) | ((uint32_t)k << sh);
-            fw |= punot << (8 + j);
-          }
-          fw |= (live_j & (hc | big)) << j;  // adopts, or merges with same > n - k: decider
         }
-      } else {  // the general schedule: each slot's HO set drawn in full
+        if (crashr && pk_any(und)) {
+          uint32_t cw = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) cw |= CNa.w[w] ? 1u << w : 0u;
+#pragma unroll 1
+          for (int j = 0; j < W; ++j) {  // one copy of the draw: the slot index is a loop variable
+            if (!pk_any((und >> j) & 1u)) continue;
+            const int pid = P.pid(j);
+            Mask<W> S = mzero<W>();  // the crashing senders p hears
+#pragma unroll
+            for (int c2 = 0; 2 * c2 < W; ++c2) {
+              if (!((cw >> (2 * c2)) & 3u)) continue;
+              const U4 o = philox10((uint32_t)inst, (uint32_t)(inst >> 32), (uint32_t)k,
+                                    (uint32_t)pid + ((uint32_t)c2 << 16), (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+              S.w[2 * c2] = CNa.w[2 * c2] & ((uint64_t)o.x | ((uint64_t)o.y << 32));
+              if (2 * c2 + 1 < W) S.w[2 * c2 + 1] = CNa.w[2 * c2 + 1] & ((uint64_t)o.z | ((uint64_t)o.w << 32));
+            }
+            const bool self = selfb && mtest(act, pid);
+            const Mask<W> M = mor(Ulo, S);
+            const uint32_t hc = (many(mand(M, Dm)) || (self && mtest(Dm, pid))) ? 1u : 0u;
+            const uint32_t big = mpopc(M) + ((self && !mtest(M, pid)) ? 1 : 0) > need ? 1u : 0u;
+            hcb = (hcb & ~(1u << j)) | (hc << j);
+            bigb = (bigb & ~(1u << j)) | (big << j);
+          }
+        }
+      } else {  // the general schedule: each slot's HO set drawn in full (one copy of the draw)
 #pragma unroll 1
         for (int j = 0; j < W; ++j) {
-          const int pid = P.pid(j);
-          const uint32_t sh = 8u * (uint32_t)j;
-          const bool halted = ((hr >> sh) & 0xFFu) != 0xFFu;
-          const uint32_t decider = (fw >> j) & 1u;
-          const uint32_t live_j = (pid < n ? 1u : 0u) & (halted ? 0u : 1u) & (1u - decider);
-          const Mask<W> M = mand(sc.ho(k, pid, good, goodS, CB, CN), act);
-          const uint32_t hc = many(mand(M, Dm)) ? 1u : 0u;
-          const uint32_t big = mpopc(M) > need ? 1u : 0u;
-          if (!halted && decider) {  // decide(pick(t)) = pu; exitAtEndOfRound (KSetAgreement.scala:48-50)
-            hr = (hr & ~(0xFFu << sh)) | ((uint32_t)k << sh);
-            fw |= punot << (8 + j);
-          }
-          fw |= (live_j & (hc | big)) << j;  // adopts, or merges with same > n - k: decider
+          const Mask<W> M = mand(sc.ho(k, P.pid(j), good, goodS, CB, CN), act);
+          hcb |= (many(mand(M, Dm)) ? 1u : 0u) << j;
+          bigb |= (mpopc(M) > need ? 1u : 0u) << j;
         }
       }
 #pragma unroll
-      for (int j = 0; j < W; ++j) al[j] = P.val[j] & (((hr >> (8 * j)) & 0xFFu) != 0xFFu ? 0u : 1u);
+      for (int j = 0; j < W; ++j) {
+        const bool halted = halt_round[j] >= 0;
+        const uint32_t decider = (fw >> j) & 1u;
+        const uint32_t live_j = P.val[j] & (halted ? 0u : 1u) & (1u - decider);
+        if (!halted && decider) {  // decide(pick(t)) = pu; exitAtEndOfRound (KSetAgreement.scala:48-50)
+          decision[j] = pu;
+          fw |= punot << (8 + j);
+          halt_round[j] = k;
+        }
+        fw |= (live_j & ((hcb | bigb) >> j) & 1u) << j;  // adopts, or merges with same > n - k: decider
+        al[j] = P.val[j] & (halt_round[j] >= 0 ? 0u : 1u);
+      }
       act = P.ballot(al);
     }
     check(k + 1);
     pt.mark(live ? 4 : 5);
-  }
-  // final x = pick(t): a process halted before the hand-off decided pick of its own (frozen) t,
-  // every other process holds the common t
-  int32_t decision[W], halt_round[W], mainx[W];
-#pragma unroll
-  for (int j = 0; j < W; ++j) {
-    const uint32_t b = (hr >> (8 * j)) & 0xFFu;
-    halt_round[j] = b == 0xFFu ? -1 : (int32_t)b;
-    decision[j] = b == 0xFFu ? 0 : (((hb >> j) & 1u) ? decl[j] : pu);
-    mainx[j] = ((hb >> j) & 1u) ? decl[j] : pu;
   }
   pk_finish<W>(P, a, i, ck, 2, decision, halt_round, halt_round, mainx, bc);
   pt.mark(3);
@@ -754,9 +741,11 @@ PSG_DEV void kset_tail(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst
 #define PSG_KSET_SPLIT 1  // 1: general rounds here, the uniform-t tail in kset_tail_kernel; 0: one kernel
 #endif
 template <int W, bool HAND>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_KSET_PK_WPE))) kset_packed_kernel(KArgs a) {
+__global__ void __launch_bounds__(64 * KsStage<W>::kWaves) __attribute__((amdgpu_waves_per_eu(PSG_KSET_PK_WPE)))
+kset_packed_kernel(KArgs a) {
+  static_assert(64 * KsStage<W>::kWaves == 256, "launched with 256-thread blocks (launch_w)");
   __shared__ BlockCounters bc;
-  __shared__ KsPk<W> L[4];
+  __shared__ KsPk<W> L[KsStage<W>::kWaves];
   __shared__ KsStage<W> S;
   __shared__ int32_t x0tab[4][X0Set<W>::kSlots];
   counters_init(&bc);
@@ -770,7 +759,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PSG_KS
   InstanceQueue<1> Q;
   for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
-    kset_packed<W, HAND>(P, a, i, inst, L[grp], S, grp * KsStage<W>::kBufs / 4, x0tab[grp], &bc, pt);
+    kset_packed<W, HAND>(P, a, i, inst, L[grp], S, grp * KsStage<W>::kBufs / KsStage<W>::kWaves, x0tab[grp], &bc, pt);
   }
   pt.flush(a.counters, P.lane);
   __syncthreads();

@@ -58,13 +58,28 @@ GenOptions parse_options(const std::string& t) {
     if (tok == "nosym") o.symmetric = false;
     else if (tok == "nosplit") o.split = false;
     else if (tok.size() > 1 && tok[0] == 'D') {
-      const std::string name = tok.substr(1, tok.find('=') == std::string::npos ? std::string::npos : tok.find('=') - 1);
+      const size_t eq = tok.find('=');
+      const std::string name = tok.substr(1, eq == std::string::npos ? std::string::npos : eq - 1);
+      const std::string value = eq == std::string::npos ? std::string() : tok.substr(eq + 1);
       if (name.empty() || name.find_first_not_of("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789_") !=
                               std::string::npos)
         throw SpecError("PSG_SPEC_OPTIONS: bad define " + tok);
+      // every knob is an integer: the value never carries source text (a newline would paste
+      // arbitrary code into the generated module)
+      if (value.find_first_not_of("0123456789") != std::string::npos && !(value.size() > 1 && value[0] == '-' &&
+                                                                          value.find_first_not_of("0123456789", 1) == std::string::npos))
+        throw SpecError("PSG_SPEC_OPTIONS: define " + name + " takes an integer value");
 #ifndef PSG_PROBE_BUILD
-      // ablation / A-B switches of probe builds change results: never in a product module
-      if (name.compare(0, 6, "PSG_AB") == 0) throw SpecError("PSG_SPEC_OPTIONS: " + name + " needs a probe build");
+      // allow-list: the profiling switch and the knobs whose settings are exact alternatives
+      // (occupancy targets, instance-queue chunking, instruction-selection forms); anything
+      // else (PSG_MAX_CHECKS, PSG_FUSED_MODULE, probe switches) would change what a product
+      // module computes
+      static const char* const kKnobs[] = {"PSG_PHASE_TIMERS", "PSG_PHILOX_OPAQUE_KEYS", "PSG_PHILOX_MAD64",
+                                           "PSG_XSHFL_MASK",   "PSG_QUEUE_CHUNK",        "PSG_QUEUE_CHUNK_WIDE",
+                                           "PSG_MAJ_BITVOTE",  "PSG_BO_FLAGS_DPP"};
+      bool ok = name.size() > 8 && name.compare(0, 4, "PSG_") == 0 && name.compare(name.size() - 4, 4, "_WPE") == 0;
+      for (const char* k : kKnobs) ok = ok || name == k;
+      if (!ok) throw SpecError("PSG_SPEC_OPTIONS: " + name + " is not a generator knob (or needs a probe build)");
 #endif
       o.defines.push_back(tok.substr(1));
     } else if (!tok.empty()) throw SpecError("PSG_SPEC_OPTIONS: unknown option " + tok);
@@ -1296,6 +1311,74 @@ std::set<std::string>& interned() {  // module paths handed out (valid until the
   return s;
 }
 
+// The compiler the modules are built with. A process may already hold another HIP toolchain under
+// the same sonames: PyTorch's wheel bundles its own libamdhip64 / libhiprtc / libamd_comgr (ROCm
+// 7.0 here), and once `import torch` has loaded them, libpsg's libhiprtc.so.7 and the comgr that
+// hiprtc loads by name resolve to torch's copies. Both toolchains report the same hiprtcVersion,
+// so modules compiled by either shared one cache key, and they differ: ROCm 7.0's comgr gives the
+// fused LastVoting kernel 416 B of scratch (187 SGPR spills) where the image's ROCm 7.2 gives none
+// — round 5's one-process configuration run loaded such a module and ran fused LastVoting 3.4x
+// slower (profiles/r5_configs: Scratch_Size 416 in the dispatch record). So the
+// image's comgr and hiprtc (PSG_ROCM_LIB, default /opt/rocm/lib) are loaded into a link-map
+// namespace of their own (dlmopen), comgr first, whatever the process has loaded, and the cache
+// key carries the files they came from. If that fails, the process's own hiprtc is used and its
+// file is in the key.
+struct RtcApi {
+  decltype(&hiprtcCreateProgram) create = nullptr;
+  decltype(&hiprtcCompileProgram) compile = nullptr;
+  decltype(&hiprtcGetProgramLogSize) log_size = nullptr;
+  decltype(&hiprtcGetProgramLog) log = nullptr;
+  decltype(&hiprtcGetCodeSize) code_size = nullptr;
+  decltype(&hiprtcGetCode) code = nullptr;
+  decltype(&hiprtcDestroyProgram) destroy = nullptr;
+  std::string ident;  // the compiler's files (cache key)
+};
+
+std::string file_ident(const std::string& path) {
+  char real[4096];
+  const std::string rp = realpath(path.c_str(), real) ? std::string(real) : path;
+  struct stat st;
+  return rp + ":" + (stat(rp.c_str(), &st) == 0 ? std::to_string((long long)st.st_size) : std::string("?"));
+}
+
+const RtcApi& rtc_api() {
+  static const RtcApi api = [] {
+    RtcApi a;
+    const std::string dir = env_or("PSG_ROCM_LIB", "/opt/rocm/lib");
+    const std::string comgr = dir + "/libamd_comgr.so.3", rtc = dir + "/libhiprtc.so.7";
+    void* hc = dlmopen(LM_ID_NEWLM, comgr.c_str(), RTLD_NOW | RTLD_LOCAL);
+    Lmid_t lm = 0;
+    void* hr = nullptr;
+    if (hc && dlinfo(hc, RTLD_DI_LMID, &lm) == 0) hr = dlmopen(lm, rtc.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (hr) {
+      a.create = (decltype(a.create))dlsym(hr, "hiprtcCreateProgram");
+      a.compile = (decltype(a.compile))dlsym(hr, "hiprtcCompileProgram");
+      a.log_size = (decltype(a.log_size))dlsym(hr, "hiprtcGetProgramLogSize");
+      a.log = (decltype(a.log))dlsym(hr, "hiprtcGetProgramLog");
+      a.code_size = (decltype(a.code_size))dlsym(hr, "hiprtcGetCodeSize");
+      a.code = (decltype(a.code))dlsym(hr, "hiprtcGetCode");
+      a.destroy = (decltype(a.destroy))dlsym(hr, "hiprtcDestroyProgram");
+    }
+    if (a.create && a.compile && a.log_size && a.log && a.code_size && a.code && a.destroy) {
+      a.ident = "isolated " + file_ident(rtc) + " " + file_ident(comgr);
+      return a;
+    }
+    a = RtcApi();  // the process's own hiprtc (whichever copy the dynamic linker bound)
+    a.create = &hiprtcCreateProgram;
+    a.compile = &hiprtcCompileProgram;
+    a.log_size = &hiprtcGetProgramLogSize;
+    a.log = &hiprtcGetProgramLog;
+    a.code_size = &hiprtcGetCodeSize;
+    a.code = &hiprtcGetCode;
+    a.destroy = &hiprtcDestroyProgram;
+    Dl_info info;
+    a.ident = std::string("process ") +
+              (dladdr((const void*)&hiprtcCompileProgram, &info) && info.dli_fname ? file_ident(info.dli_fname) : "?");
+    return a;
+  }();
+  return api;
+}
+
 int compile_module(const std::string& src, int alg, bool fused, const char* cache_dir, std::string& path,
                    std::string& err) {
   const std::string lib = lib_dir();
@@ -1309,11 +1392,14 @@ int compile_module(const std::string& src, int alg, bool fused, const char* cach
     hdr_names.push_back("psg_kernels.hpp");
     hdr_names.push_back("psg_packed.hpp");
   }
-  // the cache key: the source, the kernel headers and psg.h, and the compiler's identity
-  // (hiprtc version and options), so a module built by another toolchain is never reused
+  // the cache key: the source, the kernel headers and psg.h, and the compiler's identity (the
+  // files of the hiprtc and comgr that compile it, and the options), so a module built by another
+  // toolchain is never reused
+  const RtcApi& R = rtc_api();
   int rtc_major = 0, rtc_minor = 0;
   (void)hiprtcVersion(&rtc_major, &rtc_minor);
-  const std::string toolchain = "hiprtc " + S(rtc_major) + "." + S(rtc_minor) + " --offload-arch=gfx950 -O3 -std=c++17";
+  const std::string toolchain = "hiprtc " + S(rtc_major) + "." + S(rtc_minor) + " " + R.ident +
+                                " --offload-arch=gfx950 -O3 -std=c++17";
   Sha256 h;
   h.update(toolchain);
   h.update(src);
@@ -1340,27 +1426,27 @@ int compile_module(const std::string& src, int alg, bool fused, const char* cach
       if (!d.empty()) (void)::mkdir(d.c_str(), 0755);
     }
   hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "spec.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+  if (R.create(&prog, src.c_str(), "spec.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
     err = "native spec: hiprtcCreateProgram failed";
     return PSG_EIO;
   }
   const std::string oi = "-I" + csrc, oj = "-I" + inc;
   const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", oi.c_str(), oj.c_str()};
-  const hiprtcResult rc = hiprtcCompileProgram(prog, 5, opts);
+  const hiprtcResult rc = R.compile(prog, 5, opts);
   if (rc != HIPRTC_SUCCESS) {
     size_t ls = 0;
-    hiprtcGetProgramLogSize(prog, &ls);
+    R.log_size(prog, &ls);
     std::string log(ls, '\0');
-    if (ls) hiprtcGetProgramLog(prog, &log[0]);
-    hiprtcDestroyProgram(&prog);
+    if (ls) R.log(prog, &log[0]);
+    R.destroy(&prog);
     err = "native spec compile failed:\n" + log.substr(log.size() > 4000 ? log.size() - 4000 : 0);
     return PSG_EINVAL;
   }
   size_t cs = 0;
-  hiprtcGetCodeSize(prog, &cs);
+  R.code_size(prog, &cs);
   std::string code(cs, '\0');
-  if (cs) hiprtcGetCode(prog, &code[0]);
-  hiprtcDestroyProgram(&prog);
+  if (cs) R.code(prog, &code[0]);
+  R.destroy(&prog);
   const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
   {
     std::ofstream out(tmp, std::ios::binary);

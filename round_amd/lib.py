@@ -11,6 +11,7 @@ torch already loaded (same SONAME), keeping one HIP runtime per process.
 """
 import ctypes as C
 import os
+import threading
 import sys
 
 from . import abi
@@ -380,20 +381,29 @@ def spec_from_text(text, alg=0):
         L.psg_spec_release(C.byref(cp))
 
 
+_spec_opts = threading.local()  # the option string this thread last set through _SpecOptions
+
+
 class _SpecOptions:
     """The generator's options (psg.h psg_spec_set_options) on the calling thread for the
-    duration of one call; the environment is not touched, so threads never share them."""
+    duration of one call; the environment is not touched, so threads never share them. On exit
+    the thread's previous options are restored (nested calls keep the outer ones); None (the
+    library falls back to PSG_SPEC_OPTIONS) only when nothing was set before."""
 
     def __init__(self, options):
         self.options = ",".join(options)
 
     def __enter__(self):
         from . import formula
+        self.prev = getattr(_spec_opts, "value", None)
         if load().psg_spec_set_options(self.options.encode()) != 0:
+            load().psg_spec_set_options(None if self.prev is None else self.prev.encode())
             raise formula.FormulaError(f"invalid generator options {self.options!r}")
+        _spec_opts.value = self.options
 
     def __exit__(self, *exc):
-        load().psg_spec_set_options(None)
+        load().psg_spec_set_options(None if self.prev is None else self.prev.encode())
+        _spec_opts.value = self.prev
 
 
 def spec_compile_native(text, alg=0, fused=False, n=0, cache_dir=None, options=()):

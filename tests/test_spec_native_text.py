@@ -10,6 +10,7 @@ and fused; the DSL -> text -> DSL round trip lowers to the same source; a hiprtc
 object whose program equals psg_spec_from_text's. GPU tests: the library-compiled fused module's
 results equal the built-in checker's, word for word.
 """
+import ctypes as C
 import os
 
 import pytest
@@ -70,7 +71,7 @@ def test_generator_options_are_per_thread():
             (lib.spec_native_source, t_otr, abi.PSG_ALG_OTR, ("DPSG_PHASE_TIMERS=1",)),
             (lib.spec_rewrite_text, t_lv, abi.PSG_ALG_LAST_VOTING, ()),
             (lib.spec_rewrite_text, t_lv, abi.PSG_ALG_LAST_VOTING, ("nosplit",)),
-            (lib.spec_native_source, t_lv, abi.PSG_ALG_LAST_VOTING, ("nosym", "DPSG_X=3")),
+            (lib.spec_native_source, t_lv, abi.PSG_ALG_LAST_VOTING, ("nosym", "DPSG_QUEUE_CHUNK=3")),
             (lib.spec_rewrite_text, t_otr, abi.PSG_ALG_OTR, ("nosplit",))]
     want = [fn(t, alg, options=o) for fn, t, alg, o in jobs]
     got = [[] for _ in jobs]
@@ -96,6 +97,27 @@ def test_generator_options_are_per_thread():
     assert want[0] != want[1] and want[4] != want[5] and want[3].startswith("#define PSG_PHASE_TIMERS 1\n")
 
 
+def test_nested_options_restore_the_outer_ones():
+    """_SpecOptions restores the thread's previous options on exit: an inner call
+    with its own options leaves the outer call's options in force."""
+    t = F.to_text(F.otr_spec())
+    want = lib.spec_native_source(t, abi.PSG_ALG_OTR, options=["nosym"])
+    with lib._SpecOptions(["nosym"]):
+        lib.spec_native_source(t, abi.PSG_ALG_OTR, options=["DPSG_PHASE_TIMERS=1"])
+        # the outer options are back: a call with no options of its own sees nosym
+        n = C.c_size_t(0)
+        err = C.create_string_buffer(512)
+        L = lib.load()
+        assert L.psg_spec_native_source(t.encode(), abi.PSG_ALG_OTR, 0, 0, None, C.byref(n), err, 512) == abi.PSG_ERANGE
+        buf = C.create_string_buffer(n.value)
+        assert L.psg_spec_native_source(t.encode(), abi.PSG_ALG_OTR, 0, 0, buf, C.byref(n), err, 512) == abi.PSG_OK
+        assert buf.value.decode() == want
+    assert "spec::uniform<" in lib.spec_native_source(t, abi.PSG_ALG_OTR)
+    with pytest.raises(F.FormulaError):
+        with lib._SpecOptions(["nosym"]):
+            lib.spec_native_source(t, abi.PSG_ALG_OTR, options=["bogus"])
+
+
 def test_probe_switches_rejected():
     """A define naming a probe-build switch (PSG_AB*) never reaches a product module: from the
     per-thread setter and from the environment alike the entry points return PSG_EINVAL."""
@@ -107,6 +129,14 @@ def test_probe_switches_rejected():
     L = lib.load()
     assert L.psg_spec_set_options(b"DPSG_AB_NO_CW=1") == abi.PSG_EINVAL
     assert L.psg_spec_set_options(b"D=1") == abi.PSG_EINVAL
+    # allow-list and integer values only: no result-changing define, no source text
+    assert L.psg_spec_set_options(b"DPSG_MAX_CHECKS=3") == abi.PSG_EINVAL
+    assert L.psg_spec_set_options(b"DPSG_FUSED_MODULE=1") == abi.PSG_EINVAL
+    assert L.psg_spec_set_options(b"DPSG_OTR_WPE=4\nint x;") == abi.PSG_EINVAL
+    assert L.psg_spec_set_options(b"DPSG_OTR_WPE=a") == abi.PSG_EINVAL
+    assert L.psg_spec_set_options(b"DPSG_OTR_WPE=-3") == abi.PSG_OK
+    assert L.psg_spec_set_options(b"DPSG_QUEUE_CHUNK=8,nosym") == abi.PSG_OK
+    assert L.psg_spec_set_options(None) == abi.PSG_OK
     # through the environment (the JVM route): a child process, rc of psg_spec_native_source
     code = ("import ctypes as C, sys; sys.path.insert(0, %r); from round_amd import lib, formula as F, abi; "
             "L = lib.load(); n = C.c_size_t(0); err = C.create_string_buffer(512); "
@@ -166,3 +196,35 @@ def test_text_fused_module_equals_builtin_and_python(alg, mk, n, count, kw):
                      [(s.digest, tuple(s.first_fail), s.term_round) for s in r.per_instance])
     assert key(rc) == key(rp)
     assert key(rc) == key(builtin)
+
+
+_TOOLCHAIN_PROBE = r"""
+import hashlib, os, sys
+if sys.argv[1] == "torch":
+    import torch  # noqa: F401  (the process now holds torch's bundled HIP libraries)
+sys.path.insert(0, sys.argv[3])
+from round_amd import lib, formula as F, abi
+p = lib.spec_compile_native(F.to_text(F.otr_spec()), abi.PSG_ALG_OTR, False, 0, cache_dir=sys.argv[2])
+maps = open('/proc/self/maps').read()
+comgr = sorted(set(l.split()[-1] for l in maps.splitlines() if 'amd_comgr' in l))
+print(os.path.basename(p.module_path), hashlib.sha256(open(p.module_path, 'rb').read()).hexdigest(), '|'.join(comgr))
+"""
+
+
+def test_module_toolchain_independent_of_torch(tmp_path):
+    """A module compiled in a process that imported torch first (which binds torch's bundled
+    ROCm 7.0 hiprtc / comgr under the same sonames) is the module a plain process compiles: the
+    generator loads the image's comgr and hiprtc into a namespace of their own (psg_spec_gen.cpp
+    rtc_api). Round 5's one-process config run had loaded a torch-compiled fused LastVoting
+    module with 416 B of scratch, 3.4x slower."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for mode in ("plain", "torch"):
+        r = subprocess.run([sys.executable, "-c", _TOOLCHAIN_PROBE, mode, str(tmp_path / mode), root],
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[mode] = r.stdout.split()
+    assert out["plain"][:2] == out["torch"][:2]  # same cache key, same code object bytes
+    assert any(p.startswith("/opt/rocm") for p in out["torch"][2].split("|")), out["torch"]
