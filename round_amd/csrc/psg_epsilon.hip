@@ -36,6 +36,77 @@ PSG_DEV int32_t d2i(double d) {
   return (int32_t)d;
 }
 
+// log(x): OCML's __ocml_log_f64 (ROCm device libs, ocml.bc), restated operation for operation so
+// the result is the same double. Inlined from the library, its nine 64-bit literals are
+// loop-invariant: the compiler hoists them out of the instance loop into VGPR pairs that stay live
+// across every round and spill (96 B of scratch at 6 waves/SIMD, round 5). Here each literal passes
+// an opaque copy at its use, so it is materialized where log runs (once per instance, maxR).
+template <uint64_t BITS>
+PSG_DEV double lit64() {  // the double with these bits, materialized here (two v_mov_b32 in asm)
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t lo, hi;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(lo) : "n"((int32_t)(uint32_t)BITS));
+  asm volatile("v_mov_b32 %0, %1" : "=v"(hi) : "n"((int32_t)(uint32_t)(BITS >> 32)));
+  return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+#else
+  return __builtin_bit_cast(double, BITS);
+#endif
+}
+PSG_DEV double log_ocml(double x) {
+#pragma clang fp contract(off)
+  int e0;
+  const double m0 = __builtin_frexp(x, &e0);
+  const bool lo = m0 < lit64<0x3FE5555555555555ULL>();
+  const double m = m0 * (lo ? 2.0 : 1.0);
+  const int e = e0 + (lo ? -1 : 0);
+  const double a = m + -1.0, b = m + 1.0;
+  const double bl = m - (b + -1.0);
+  const double r0 = __builtin_amdgcn_rcp(b);
+  const double r1 = fma(fma(-b, r0, 1.0), r0, r0);
+  const double r = fma(fma(-b, r1, 1.0), r1, r1);
+  const double q0 = a * r;  // (a / b) in double-double: q0 + q1
+  const double p = b * q0;
+  const double pl = fma(q0, bl, fma(q0, b, -p));
+  const double s = p + pl;
+  const double sl = pl - (s - p);
+  const double d = a - s;
+  const double dl = ((a - d) - s) - sl;
+  const double q1c = r * (d + dl);
+  const double q = q0 + q1c;
+  const double ql = q1c - (q - q0);
+  const double z = q * q;
+  double t = fma(z, lit64<0x3FC3AB76BF559E2BULL>(), lit64<0x3FC385386B47B09AULL>());
+  t = fma(z, t, lit64<0x3FC7474DD7F4DF2EULL>());
+  t = fma(z, t, lit64<0x3FCC71C016291751ULL>());
+  t = fma(z, t, lit64<0x3FD249249B27ACF1ULL>());
+  t = fma(z, t, lit64<0x3FD99999998EF7B6ULL>());
+  t = fma(z, t, lit64<0x3FE5555555555780ULL>());
+  const double h2 = __builtin_ldexp(q, 1), l2 = __builtin_ldexp(ql, 1);
+  const double w = (q * z) * t;
+  const double u = h2 + w;
+  const double ul = l2 + (w - (u - h2));
+  const double v = u + ul;
+  const double vl = ul - (v - u);
+  const double fe = (double)e, ln2h = lit64<0x3FE62E42FEFA39EFULL>();
+  const double k0 = fe * ln2h;
+  const double kl = fma(fe, lit64<0x3C7ABC9E3B39803FULL>(), fma(fe, ln2h, -k0));
+  const double k = k0 + kl;
+  const double kr = kl - (k - k0);
+  const double s1 = k + v;
+  const double s1b = s1 - k;
+  const double s1l = (v - s1b) + (k - (s1 - s1b));
+  const double s2 = kr + vl;
+  const double s2b = s2 - kr;
+  const double s2l = (vl - s2b) + (kr - (s2 - s2b));
+  const double s3 = s2 + s1l;
+  const double s4 = s1 + s3;
+  const double res = s4 + (s2l + (s3 - (s4 - s1)));
+  const double ax = __builtin_fabs(x);
+  double out = ax == __builtin_inf() ? x : res;
+  out = x < 0.0 ? __builtin_nan("") : out;
+  return x == 0.0 ? -__builtin_inf() : out;
+}
+
 PSG_DEV int32_t fold32d(double d) {
   const uint64_t b = (uint64_t)__double_as_longlong(d);
   return (int32_t)(uint32_t)(b ^ (b >> 32));
@@ -196,7 +267,7 @@ epsilon_kernel(KArgs a) {
   const int n = a.n;
   const int f = a.param;
   const double eps = a.real_param;
-  const double logc = log((double)((n - 3 * f - 1) / (2 * f) + 1));  // log(c(n-3f, 2f))
+  const double logc = log_ocml((double)((n - 3 * f - 1) / (2 * f) + 1));  // log(c(n-3f, 2f))
   const Mask<W> full = mfull<W>(n);
   double* sx = L.sx[grp];
   int32_t* spid = L.spid[grp];
@@ -333,7 +404,7 @@ epsilon_kernel(KArgs a) {
           H = mor(H, mand(M, Fl));  // halted ++ mailbox.filter(_._2._2)
           if (k == 0) {
             if (m > 0) {  // (empty V: Scala throws; left unchanged)
-              const double r1 = log((last - first) / eps) / logc;
+              const double r1 = log_ocml((last - first) / eps) / logc;
               maxR = d2i(ceil(r1));
               if (a.variant == 1) maxR = 0;  // variant 1: mutation, no approximation rounds
               if (m > 4 * f) x = e2f;  // reduce(2f, V).head

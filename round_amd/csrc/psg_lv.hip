@@ -85,11 +85,23 @@ PSG_DEV LvState<W> lv_state(Grp<W>& g, LvLds<W>& L, bool has_old, const Mask<W>&
     if constexpr (!FROZEN)
       st.irrev = !has_old || !g.any_raw((old_fl & F_DECIDED) != 0u && !(dec01 != 0u && old_decision == decision));
   }
-  st.noDec = !g.any_raw((fl & (FROZEN ? F_DECIDED : F_DECIDED | F_READY)) != 0u);  // 0 past n but F_HALTED
+  if constexpr (FROZEN) {
+    // No process is commit or ready in the quiescent tail, so the pinned processes are the
+    // deciders: noDec = no decider, the pins' witness z0 is the first decider's decision d0, and
+    // "every pinned process agrees with z0" is Agreement (`same`: exact when a witness was found,
+    // and true otherwise, as then every decision equals d0). The same terms, from the ballots above.
+    st.noDec = !st.anyD;
+    st.zAny = st.anyD;
+    st.z0 = d0;
+    st.zOk = st.same;
+    st.C = mzero<W>();
+    return st;
+  }
+  st.noDec = !g.any_raw((fl & (F_DECIDED | F_READY)) != 0u);  // 0 past n but F_HALTED
   // values pinned by (decided ==> decision == v), (commit ==> vote == v), (ready ==> vote == v):
   // z0 = the pinned value of the first pinned process (its decision if it decided, else its
   // vote), and every pinned process must agree with it
-  const uint32_t cr01 = !FROZEN && (fl & (F_COMMIT | F_READY)) ? 1u : 0u;
+  const uint32_t cr01 = (fl & (F_COMMIT | F_READY)) ? 1u : 0u;
   const Mask<W> Pm = g.ballot_any((dec01 | cr01) != 0u);
   st.zAny = many(Pm);
   st.z0 = 0;
@@ -103,11 +115,15 @@ PSG_DEV LvState<W> lv_state(Grp<W>& g, LvLds<W>& L, bool has_old, const Mask<W>&
     st.z0 = g.bcast(zl, L.votes, mfirst(Pm));
     st.zOk = !g.any_raw(((dec01 & ne01(decision, st.z0)) | (cr01 & ne01(vote, st.z0))) != 0u);
   }
-  st.C = FROZEN ? mzero<W>() : g.ballot_any((fl & F_COMMIT) != 0u);
+  st.C = g.ballot_any((fl & F_COMMIT) != 0u);
   return st;
 }
 
-template <int W>
+// FROZEN: a check point of the quiescent tail, which starts at a phase boundary 4φ (φ >= 1) where
+// every ts <= φ - 1 (ts only takes a phase number in that phase's R1), while every tail check
+// point has r/4 >= φ: so no process has ts == r/4 and (i.ts == r/4) ==> coord.commit holds by the
+// tail's invariant, as its commit / ready terms are 0.
+template <int W, bool FROZEN = false>
 PSG_DEV void lv_check_at(Grp<W>& g, LvLds<W>& L, Checks& ck, const LvState<W>& st, int c, int32_t r4, int coord,
                          int n, int32_t x, int32_t ts) {
   // r4 = c / 4, coord = (c / 4) % n: maintained incrementally by the caller (a runtime `% n`
@@ -116,7 +132,7 @@ PSG_DEV void lv_check_at(Grp<W>& g, LvLds<W>& L, Checks& ck, const LvState<W>& s
   // (Invariant0 reads maj only when keepInit holds and some process decided or is ready)
   if (c > 0 && st.zOk && st.keep && !st.noDec &&
       // (i.ts == r/4) ==> coord.commit
-      (mtest(st.C, coord) || !g.any_raw(ts == r4))) {  // ts = -1 past n
+      (FROZEN || mtest(st.C, coord) || !g.any_raw(ts == r4))) {  // ts = -1 past n
     // exists t <= r/4: A_t = {i : i.ts >= t}, |A_t| > n/2, all x over A_t equal (to the pinned
     // value). The sets A_t shrink as t grows, and "all x over A equal (to z0)" holds on every
     // non-empty subset of a set it holds on, so the exists holds iff it holds at the largest
@@ -154,7 +170,7 @@ PSG_DEV void lv_check(Grp<W>& g, LvLds<W>& L, Checks& ck, int c, int32_t r4, int
                       uint32_t old_fl, int32_t old_decision, uint32_t xin01, uint32_t din01) {
   const LvState<W> st =
       lv_state<W, FROZEN>(g, L, has_old, full, x, ts, vote, decision, fl, old_fl, old_decision, xin01, din01);
-  lv_check_at<W>(g, L, ck, st, c, r4, coord, n, x, ts);
+  lv_check_at<W, FROZEN>(g, L, ck, st, c, r4, coord, n, x, ts);
 }
 
 // The coordinator's HO mask (uniform).

@@ -89,7 +89,10 @@ PSG_DEV void otr_check(Grp<W>& g, OtrLds<W>& L, const X0Set<W>& X0, Checks& ck, 
     same = !many(mand(D, g.ballot(decision != d0)));
     if (has_old) irrev = !many(mandn(g.ballot(old01 != 0u), mand(D, g.ballot(old_decision == decision))));
   }
-  const int32_t ref = anyD ? d0 : majority_candidate<W>(g, x);
+  // the vote count's value: d0 once someone decided; before that OTR reads the count only as
+  // cnt == n (Invariant1; Invariant0 is keepInit alone with no decision), which holds iff every
+  // x equals process 0's — the majority candidate is needed only for OTR2's e0 (and W > 1)
+  const int32_t ref = anyD ? d0 : ((!V2 && W == 1) ? readlane32(x, 0) : majority_candidate<W>(g, x));
   const int cnt = mpopc(g.ballot((valid01 & eq01(x, ref)) != 0u));
   const bool condv = !anyD || same;
   const bool e0 = condv && cnt > sthr;
