@@ -1306,10 +1306,12 @@ struct NoHook {
   };
 };
 
-// Is the process state of every check point needed (trace or fused Spec)?
-template <class SH>
+// Is the process state of every check point needed (trace or fused Spec)? TR = false: the
+// launch has no Spec-program trace (known at compile time: the instantiation the library's
+// built-in-checker launches use, which then holds no trace pointers or field masks)
+template <class SH, bool TR = true>
 PSG_DEV bool tracing(const KArgs& a) {
-  return SH::kFused || a.trace != nullptr;
+  return SH::kFused || (TR && a.trace != nullptr);
 }
 
 // One check point's process state: to the fused Spec, else to the trace.

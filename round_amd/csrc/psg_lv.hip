@@ -224,7 +224,7 @@ struct CoordWords {
 
 // Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
 // fused Spec module (round_amd/formula.py compile_native(fused=True)).
-template <int W, bool XHO, class SH = NoHook>
+template <int W, bool XHO, class SH = NoHook, bool TR = true>
 PSG_DEV void lv_body(const KArgs& a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[Grp<W>::kXb];
@@ -275,7 +275,7 @@ PSG_DEV void lv_body(const KArgs& a) {
       emit_state<W, SH>(sh, g, a, i, c, x, (fl & F_DECIDED) ? 1 : 0, decision, ts, (fl & F_READY) ? 1 : 0,
                         (fl & F_COMMIT) ? 1 : 0, vote, 0, hs, frozen);
     };
-    if (tracing<SH>(a)) trace(0, n);
+    if (tracing<SH, TR>(a)) trace(0, n);
     pt.mark(0);
 
     // one round of slot RS = k mod 4 (compile time: each slot's step and check specialized)
@@ -367,7 +367,7 @@ PSG_DEV void lv_body(const KArgs& a) {
       if constexpr (!SH::kFused)
         lv_check<W>(g, L, ck, k + 1, RS == 3 ? phase + 1 : phase, RS == 3 ? cnx : cph, true, n, full, x, ts, vote,
                     decision, fl, old_fl, old_decision, xin, din);
-      if (tracing<SH>(a)) trace(k + 1, (old_fl & F_HALTED) ? n : hs);
+      if (tracing<SH, TR>(a)) trace(k + 1, (old_fl & F_HALTED) ? n : hs);
       pt.mark(many(act) ? 4 : 5);
     };
     // Quiescent tail. At a phase boundary past round 0, once at most n/2 processes are not halted
@@ -379,7 +379,7 @@ PSG_DEV void lv_body(const KArgs& a) {
     // check point (with old = current: the Irrevocability witness is 0 by algebra, as in OTR's
     // frozen tail). Not taken when a trace or the fused Spec reads |mailbox|.
     const bool hs_read = SH::kFused ? ((SH::kFields >> PSG_FIELD_HOSIZE) & 1u) != 0u
-                                    : (a.trace != nullptr && ((a.trace_fields >> PSG_FIELD_HOSIZE) & 1u));
+                                    : (TR && a.trace != nullptr && ((a.trace_fields >> PSG_FIELD_HOSIZE) & 1u));
     const bool qok = a.variant == 0 && !hs_read;
     int kq = a.R;
     for (int k0 = 0; k0 < a.R; k0 += 4) {
@@ -403,7 +403,7 @@ PSG_DEV void lv_body(const KArgs& a) {
       if constexpr (!SH::kFused)
         lv_check<W, true>(g, L, ck, k + 1, RS == 3 ? phase + 1 : phase, RS == 3 ? cnx : cph, true, n, full, x, ts,
                           vote, decision, fl, fl, decision, xin, din);
-      if (tracing<SH>(a)) trace(k + 1, n, true);
+      if (tracing<SH, TR>(a)) trace(k + 1, n, true);
       if (RS == 3) {
         ++phase;
         cph = cnx;
@@ -422,17 +422,18 @@ PSG_DEV void lv_body(const KArgs& a) {
 #ifndef PSG_LV_WPE
 #define PSG_LV_WPE 6
 #endif
-template <int W, bool XHO, class SH = NoHook>
+template <int W, bool XHO, class SH = NoHook, bool TR = true>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? PSG_LV_WPE : 1)))
 lv_kernel(KArgs a) {
-  lv_body<W, XHO, SH>(a);
+  lv_body<W, XHO, SH, TR>(a);
 }
 
 #ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
   if (a.ho_in) hipLaunchKernelGGL((lv_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
-  else hipLaunchKernelGGL((lv_kernel<W, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  else if (a.trace) hipLaunchKernelGGL((lv_kernel<W, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  else hipLaunchKernelGGL((lv_kernel<W, false, NoHook, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -448,10 +449,10 @@ hipError_t launch_lv(const KArgs& a, int W, int grid, hipStream_t s) {
 
 const void* lv_kernel_ptr(int W) {
   switch (W) {
-    case 1: return (const void*)lv_kernel<1, false>;
-    case 2: return (const void*)lv_kernel<2, false>;
-    case 3: return (const void*)lv_kernel<3, false>;
-    case 4: return (const void*)lv_kernel<4, false>;
+    case 1: return (const void*)lv_kernel<1, false, NoHook, false>;
+    case 2: return (const void*)lv_kernel<2, false, NoHook, false>;
+    case 3: return (const void*)lv_kernel<3, false, NoHook, false>;
+    case 4: return (const void*)lv_kernel<4, false, NoHook, false>;
   }
   return nullptr;
 }

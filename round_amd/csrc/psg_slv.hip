@@ -57,7 +57,7 @@ PSG_DEV Mask<W> slv_ho_of(Grp<W>& g, SlvLds<W>& L, const Mask<W>& ho, int c) {
 
 // Kernel body; SH = NoHook for the library's kernels, spec::SpecHook<GenSpec> in a
 // fused Spec module (round_amd/formula.py compile_native(fused=True)).
-template <int W, bool XHO, class SH = NoHook>
+template <int W, bool XHO, class SH = NoHook, bool TR = true>
 PSG_DEV void slv_body(const KArgs& a) {
   __shared__ BlockCounters bc;
   __shared__ uint64_t xb[Grp<W>::kXb];
@@ -108,7 +108,7 @@ PSG_DEV void slv_body(const KArgs& a) {
       emit_state<W, SH>(sh, g, a, i, c, x, (fl & S_DECIDED) ? 1 : 0, decision, ts, 0, (fl & S_COMMIT) ? 1 : 0, vote, 0, hs,
                         frozen);
     };
-    if (tracing<SH>(a)) trace(0, n);
+    if (tracing<SH, TR>(a)) trace(0, n);
 
     // one round of slot RS = k mod 3 (compile time: each slot's step specialized)
     auto round = [&](const int k, auto RSc) {
@@ -184,7 +184,7 @@ PSG_DEV void slv_body(const KArgs& a) {
         }
       }
       if constexpr (!SH::kFused) check(k + 1);
-      if (tracing<SH>(a)) trace(k + 1, (fl_start & S_HALTED) ? n : hs);
+      if (tracing<SH, TR>(a)) trace(k + 1, (fl_start & S_HALTED) ? n : hs);
     };
     // Quiescent tail (as lv_body's). At a phase boundary, once at most n/2 processes are not
     // halted and none of them is commit, no process can take an effective step again: R0's
@@ -194,7 +194,7 @@ PSG_DEV void slv_body(const KArgs& a) {
     // run no step; the check is still evaluated at every check point. Not taken when a trace or
     // the fused Spec reads |mailbox|.
     const bool hs_read = SH::kFused ? ((SH::kFields >> PSG_FIELD_HOSIZE) & 1u) != 0u
-                                    : (a.trace != nullptr && ((a.trace_fields >> PSG_FIELD_HOSIZE) & 1u));
+                                    : (TR && a.trace != nullptr && ((a.trace_fields >> PSG_FIELD_HOSIZE) & 1u));
     const bool qok = a.variant == 0 && !hs_read;
     int kq = a.R;
     for (int k0 = 0; k0 < a.R; k0 += 3) {
@@ -211,7 +211,7 @@ PSG_DEV void slv_body(const KArgs& a) {
     }
     for (int k = kq; k < a.R; ++k) {
       if constexpr (!SH::kFused) check(k + 1);
-      if (tracing<SH>(a)) trace(k + 1, n, true);
+      if (tracing<SH, TR>(a)) trace(k + 1, n, true);
     }
     finish_instance<W>(g, a, i, SH::kFused ? sh.ck : ck, SH::kFused ? SH::kSlots : 2, dec_val, dec_round, halt_round, x, &bc);
   }
@@ -222,17 +222,18 @@ PSG_DEV void slv_body(const KArgs& a) {
 #ifndef PSG_SLV_WPE
 #define PSG_SLV_WPE 7  // W = 1 occupancy target: 7 measured 65.2 ms vs 6: 66.0, compiler (5): 70.5 (W2 row)
 #endif
-template <int W, bool XHO, class SH = NoHook>
+template <int W, bool XHO, class SH = NoHook, bool TR = true>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? PSG_SLV_WPE : 1)))
 slv_kernel(KArgs a) {
-  slv_body<W, XHO, SH>(a);
+  slv_body<W, XHO, SH, TR>(a);
 }
 
 #ifndef PSG_FUSED_MODULE  // host launchers (not part of a fused Spec module)
 template <int W>
 static hipError_t launch_w(const KArgs& a, int grid, hipStream_t s) {
   if (a.ho_in) hipLaunchKernelGGL((slv_kernel<W, true>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
-  else hipLaunchKernelGGL((slv_kernel<W, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  else if (a.trace) hipLaunchKernelGGL((slv_kernel<W, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
+  else hipLaunchKernelGGL((slv_kernel<W, false, NoHook, false>), dim3(grid), dim3(Geometry<W>::kThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -248,10 +249,10 @@ hipError_t launch_slv(const KArgs& a, int W, int grid, hipStream_t s) {
 
 const void* slv_kernel_ptr(int W) {
   switch (W) {
-    case 1: return (const void*)slv_kernel<1, false>;
-    case 2: return (const void*)slv_kernel<2, false>;
-    case 3: return (const void*)slv_kernel<3, false>;
-    case 4: return (const void*)slv_kernel<4, false>;
+    case 1: return (const void*)slv_kernel<1, false, NoHook, false>;
+    case 2: return (const void*)slv_kernel<2, false, NoHook, false>;
+    case 3: return (const void*)slv_kernel<3, false, NoHook, false>;
+    case 4: return (const void*)slv_kernel<4, false, NoHook, false>;
   }
   return nullptr;
 }

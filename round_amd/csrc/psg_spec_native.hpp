@@ -497,6 +497,13 @@ PSG_DEV int32_t exists_int_eq(Ctx<W>& x, const int32_t (&ev)[NE > 0 ? NE : 1],
 // otherwise the distinct values of t filtered by their count. Requires L >= 1.
 template <int W, int KEY, class Fn>
 PSG_DEV int32_t exists_int_guard(Ctx<W>& x, int32_t t, const int32_t* staged, int32_t L, Fn fn) {
+  if ((int64_t)L >= (int64_t)x.n) {
+    // held by every process (a count == n guard): the only candidate is process 0's t, no
+    // majority vote (the hand-lowered OTR check does the same before the first decision)
+    const int32_t m = x.g.bcast(t, staged, 0);
+    if (mpopc(x.g.ballot(t == m)) < L) return 0;
+    return fn(m) != 0 ? 1 : 0;
+  }
   if (2 * (int64_t)L > (int64_t)x.n) {
     // the candidate depends only on the field's values: computed once per check point
     int32_t m;
