@@ -42,7 +42,7 @@ bool is_var(const Tree& T, int e, int uid) { return T.nodes[e].k == VAR && T.nod
 // string, otherwise the environment variable PSG_SPEC_OPTIONS is read; every entry point parses
 // them into its own thread's GenOptions, so concurrent callers (JVM threads) never share state.
 struct GenOptions {
-  bool symmetric = true, split = true;
+  bool symmetric = true, split = true, frozen = true;
   std::vector<std::string> defines;
 };
 thread_local GenOptions g_opts;        // this thread's options for the generation in progress
@@ -57,6 +57,7 @@ GenOptions parse_options(const std::string& t) {
     const std::string tok = t.substr(i, j == std::string::npos ? std::string::npos : j - i);
     if (tok == "nosym") o.symmetric = false;
     else if (tok == "nosplit") o.split = false;
+    else if (tok == "nofrozen") o.frozen = false;
     else if (tok.size() > 1 && tok[0] == 'D') {
       const size_t eq = tok.find('=');
       const std::string name = tok.substr(1, eq == std::string::npos ? std::string::npos : eq - 1);
@@ -552,6 +553,11 @@ struct Gen {
   std::set<int> pvars;                       // variables bound to a process (a pid in [0, n))
   std::vector<std::pair<int, int>> uft;      // (field, tag) current / old fields the symmetric lowering reads
   std::map<std::pair<int, std::string>, int> umemo;  // (init set, C++ expression) -> member_init_u slot
+  // lowering for the kernel's frozen check points (fail_frozen): no process took a step since the
+  // previous check point, so every old field is the current one, and `facts` (field -> value) hold
+  // for every process (the algorithm's frozen-tail invariants, frozen_facts)
+  bool frozen = false;
+  std::map<int, int> facts;
 
   bool own(int uid) const {
     auto it = names.find(uid);
@@ -585,17 +591,23 @@ struct Gen {
         fields.insert(n.f);
         tags.insert(n.tag);
         const Node& p = T.nodes[n.a];
-        if (uni && n.tag != PSG_TAG_INIT) {
+        // frozen check point: old(f) is the current f; a fact field of a process (a quantified
+        // pid or coord, both in [0, n)) is its constant
+        const int tag = (frozen && n.tag == PSG_TAG_OLD) ? PSG_TAG_CUR : n.tag;
+        if (frozen && tag == PSG_TAG_CUR && facts.count(n.f) &&
+            (p.k == COORDV || (p.k == VAR && pvars.count(p.uid))))
+          return {c_int(facts.at(n.f)), false};
+        if (uni && tag != PSG_TAG_INIT) {
           // symmetric check point: every process holds process 0's value
-          add_uft(n.f, n.tag);
-          if (p.k == COORDV || (p.k == VAR && pvars.count(p.uid))) return {"x.uf(" + S(n.tag) + ", " + S(n.f) + ")", false};
+          add_uft(n.f, tag);
+          if (p.k == COORDV || (p.k == VAR && pvars.count(p.uid))) return {"x.uf(" + S(tag) + ", " + S(n.f) + ")", false};
           const Code pc = gen(n.a, in_lane, vi);
-          return {"spec::fld_uni<W>(x, " + S(n.tag) + ", " + S(n.f) + ", " + pc.first + ")", pc.second};
+          return {"spec::fld_uni<W>(x, " + S(tag) + ", " + S(n.f) + ", " + pc.first + ")", pc.second};
         }
-        if (p.k == VAR && own(p.uid)) return {"x.own(" + S(n.tag) + ", " + S(n.f) + ")", true};  // the lane's own process
+        if (p.k == VAR && own(p.uid)) return {"x.own(" + S(tag) + ", " + S(n.f) + ")", true};  // the lane's own process
         if (p.k == VAR && tuples.count(p.uid)) return {tuples[p.uid][{n.f, n.tag}], false};  // a distinct-state tuple value
         const Code pc = gen(n.a, in_lane, vi);
-        return {std::string("spec::") + (pc.second ? "fld_g" : "fld_u") + "<W>(x, " + S(n.tag) + ", " + S(n.f) + ", " +
+        return {std::string("spec::") + (pc.second ? "fld_g" : "fld_u") + "<W>(x, " + S(tag) + ", " + S(n.f) + ", " +
                     pc.first + ")",
                 pc.second};
       }
@@ -928,6 +940,20 @@ struct Gen {
 };
 
 // The native checker's source for a parsed + compiled Spec.
+// The algorithm kernels' frozen-tail invariants (fields by psg.h PSG_FIELD_*: x 0, decided 1,
+// decision 2, ts 3, ready 4, commit 5, vote 6): facts that hold for every process at a frozen
+// check point of that kernel. OTR / OTR2: the frozen tail starts when every process halted, and a
+// process halts only after deciding (Otr.scala:75-80). LastVoting: the quiescent tail starts when
+// no process is commit or ready (psg_lv.hip), and no step runs after it.
+std::map<int, int> frozen_facts(int alg) {
+  switch (alg) {
+    case PSG_ALG_OTR:
+    case PSG_ALG_OTR2: return {{PSG_FIELD_DECIDED, 1}};
+    case PSG_ALG_LAST_VOTING: return {{PSG_FIELD_READY, 0}, {PSG_FIELD_COMMIT, 0}};
+    default: return {};
+  }
+}
+
 std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
   Tree& T = P.T;
   Gen gen{T, alg != 0, alg != 0 ? alg_fields(alg) : std::set<int>{}};
@@ -1051,6 +1077,31 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
     B.slot = slot;
     return B;
   };
+  // fail() / term() bodies from the general and the symmetric-check-point blocks; the symmetric
+  // one is worth its test only with few fields to compare (uft: the fields it compares)
+  auto assemble = [&](const Block& G, const Block& U, const std::vector<std::pair<int, int>>& uft,
+                      std::vector<std::string>& body, std::vector<std::string>& term_decls) {
+    const bool has_term = G.has_term && !G.term.empty();
+    if (g_opts.symmetric && !uft.empty() && uft.size() <= 6) {
+      uint32_t cur = 0, old = 0;
+      for (auto& ft : uft) {
+        if (ft.second == PSG_TAG_CUR) cur |= 1u << ft.first;
+        else if (ft.second == PSG_TAG_OLD) old |= 1u << ft.first;
+      }
+      body.push_back("    if (spec::uniform<W, " + std::to_string(cur) + "u, " + std::to_string(old) + "u>(x)) {");
+      body.insert(body.end(), U.lines.begin(), U.lines.end());
+      body.push_back("      return fb;");
+      body.push_back("    }");
+      if (has_term) {
+        term_decls.push_back("    if (x.uni) {");
+        term_decls.insert(term_decls.end(), U.term_decls.begin(), U.term_decls.end());
+        term_decls.push_back("      return (" + U.term + ") != 0;");
+        term_decls.push_back("    }");
+      }
+    }
+    body.insert(body.end(), G.lines.begin(), G.lines.end());
+    term_decls.insert(term_decls.end(), G.term_decls.begin(), G.term_decls.end());
+  };
   Block G = block(false);
   // symmetric check points (every process holds the same value of each current / old field the
   // Spec reads): a second, scalar lowering, chosen per check point by spec::uniform
@@ -1060,26 +1111,33 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
   const bool has_term = G.has_term && !G.term.empty();
   const std::string term = G.term;
   std::vector<std::string> body, term_decls;
-  // worth its test only with few fields to compare
-  if (g_opts.symmetric && !gen.uft.empty() && gen.uft.size() <= 6) {
-    uint32_t cur = 0, old = 0;
-    for (auto& ft : gen.uft) {
-      if (ft.second == PSG_TAG_CUR) cur |= 1u << ft.first;
-      else if (ft.second == PSG_TAG_OLD) old |= 1u << ft.first;
+  assemble(G, U, gen.uft, body, term_decls);
+  // The kernel's frozen check points (SpecHook::put with frozen: no process took a step since the
+  // previous check point): the same formulas with every old field read as the current one and the
+  // algorithm's frozen-tail facts as constants (frozen_facts), so the compiler folds what they
+  // decide (Irrevocability's old.decision == decision, LastVoting's commit / ready terms). Every
+  // formula is still evaluated at every check point; only its inputs are known.
+  std::vector<std::string> fbody, fterm_decls;
+  std::string fterm;
+  bool frozen_ok = false;
+  if (g_opts.frozen && alg != 0) {
+    const auto saved_uft = gen.uft;
+    gen.uft.clear();
+    gen.frozen = true;
+    gen.facts = frozen_facts(alg);
+    try {
+      Block FG = block(false);
+      Block FU = block(true);
+      assemble(FG, FU, gen.uft, fbody, fterm_decls);
+      fterm = FG.term;
+      frozen_ok = true;
+    } catch (const SpecError&) {
+      frozen_ok = false;  // (not expected: the same tree) fail_frozen falls back to fail
     }
-    body.push_back("    if (spec::uniform<W, " + std::to_string(cur) + "u, " + std::to_string(old) + "u>(x)) {");
-    body.insert(body.end(), U.lines.begin(), U.lines.end());
-    body.push_back("      return fb;");
-    body.push_back("    }");
-    if (has_term) {
-      term_decls.push_back("    if (x.uni) {");
-      term_decls.insert(term_decls.end(), U.term_decls.begin(), U.term_decls.end());
-      term_decls.push_back("      return (" + U.term + ") != 0;");
-      term_decls.push_back("    }");
-    }
+    gen.frozen = false;
+    gen.uni = false;
+    gen.uft = saved_uft;
   }
-  body.insert(body.end(), G.lines.begin(), G.lines.end());
-  term_decls.insert(term_decls.end(), G.term_decls.begin(), G.term_decls.end());
   if (gen.max_vi > 4) throw SpecError("more than 4 nested V.exists over Int");
   uint32_t rel = 0, fmask = 0, tmask = 0;
   for (size_t s = 0; s < prog.flags.size(); ++s)
@@ -1110,7 +1168,29 @@ std::string codegen_hip(ParsedSpec& P, const Compiled& prog, int alg) {
     << "    (void)scratch;\n";
   for (auto& l : term_decls) o << l << "\n";
   o << "    return (" << (has_term && !term.empty() ? term : "0") << ") != 0;\n"
-    << "  }\n"
+    << "  }\n";
+  // frozen check points (SpecHook::put): old fields = current ones, frozen-tail facts constant
+  o << "  template <int W>\n"
+    << "  __device__ static uint32_t fail_frozen(spec::Ctx<W>& x, int32_t* scratch) {\n";
+  if (frozen_ok) {
+    o << "    (void)scratch;\n"
+      << "    uint32_t fb = 0;\n";
+    for (auto& l : fbody) o << l << "\n";
+    o << "    return fb;\n";
+  } else {
+    o << "    return fail<W>(x, scratch);\n";
+  }
+  o << "  }\n"
+    << "  template <int W>\n"
+    << "  __device__ static bool term_frozen(spec::Ctx<W>& x, int32_t* scratch) {\n";
+  if (frozen_ok) {
+    o << "    (void)scratch;\n";
+    for (auto& l : fterm_decls) o << l << "\n";
+    o << "    return (" << (has_term && !fterm.empty() ? fterm : "0") << ") != 0;\n";
+  } else {
+    o << "    return term<W>(x, scratch);\n";
+  }
+  o << "  }\n"
     << "};\n"
     << "}  // namespace psg\n"
     << "PSG_SPEC_NATIVE_KERNELS(psg::GenSpec)\n"

@@ -730,9 +730,13 @@ struct SpecHook {
         }
         if constexpr (W > 1) __syncthreads();
       }
-      uint32_t fb = S::template fail<W>(x, scratch_lds(grp));
+      // a frozen check point runs the frozen lowering (every old field is the current one, the
+      // kernel's frozen-tail facts are constants: GenSpec::fail_frozen); every formula is evaluated
+      const bool fz = frozen && c > 0;
+      uint32_t fb = fz ? S::template fail_frozen<W>(x, scratch_lds(grp)) : S::template fail<W>(x, scratch_lds(grp));
       if (c == 0) fb &= ~S::kRelational;
-      const bool term = S::kHasTerm && S::template term<W>(x, scratch_lds(grp));
+      const bool term = S::kHasTerm && (fz ? S::template term_frozen<W>(x, scratch_lds(grp))
+                                           : S::template term<W>(x, scratch_lds(grp)));
       ck.record(fb, term, c, g.lane);
       if constexpr (W > 1) __syncthreads();
     }
