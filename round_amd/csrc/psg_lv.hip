@@ -420,7 +420,7 @@ PSG_DEV void lv_body(const KArgs& a) {
 }
 
 #ifndef PSG_LV_WPE
-#define PSG_LV_WPE 6
+#define PSG_LV_WPE 7  // W = 1 occupancy target: round 6 (trace-free kernels, 94 SGPR spills) 7 measured 46.9 ms vs 6: 48.4, 8: 50.0 (C3)
 #endif
 template <int W, bool XHO, class SH = NoHook, bool TR = true>
 __global__ void __launch_bounds__(Geometry<W>::kThreads) __attribute__((amdgpu_waves_per_eu(W == 1 ? PSG_LV_WPE : 1)))

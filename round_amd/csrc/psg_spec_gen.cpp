@@ -1222,8 +1222,11 @@ std::string fused_source(int alg, const std::vector<int>& waves) {
   if (!fused_kernel(alg, src, body, pre, tail)) throw SpecError("fused lowering needs one of the integer-state algorithms");
   std::ostringstream o;
   o << "#include \"" << src << "\"  // its kernel bodies; host launchers are compiled out (PSG_FUSED_MODULE)";
-  // occupancy target of the W = 1 kernels (0: the compiler's); an empty PSG_FUSED_WPE means unset
-  int wpe = alg == PSG_ALG_LAST_VOTING ? 6 : 0;
+  // occupancy target of the W = 1 kernels (0: the compiler's); an empty PSG_FUSED_WPE means unset.
+  // Measured on MI355X (round 6, scripts/probe_fused.py): LastVoting 5/6/7/8 waves 90.0 / 84.8 /
+  // 82.8 / 81.3 ms, OTR compiler's (5) / 6 / 7 waves 38.8 / 36.4 / 37.3 ms; the extra waves cost a
+  // few spilled words outside the round loop and hide more of the checker's latency than they add
+  int wpe = alg == PSG_ALG_LAST_VOTING ? 8 : (alg == PSG_ALG_OTR || alg == PSG_ALG_OTR2) ? 6 : 0;
   if (const char* e = std::getenv("PSG_FUSED_WPE"))
     if (*e) wpe = std::atoi(e);
   for (int W : waves) {
