@@ -201,6 +201,29 @@ PSG_DEV void wave_sort_key_pid(int64_t& key, int32_t& pid, int lane) {
   if constexpr (SIZE < 64) wave_sort_key_pid<SIZE * 2>(key, pid, lane);
 }
 
+// The same network over one 64-bit word: the key's top 58 bits with the pid in the low 6
+// (distinct words, so the order is total). Sorted by that word, the list is in (key, pid)
+// order unless two keys that agree in their top 58 bits differ below them and sit against
+// their pid order — the caller checks adjacent full keys and sorts again by (key, pid) then.
+// Two 32-bit moves and one compare per step instead of three moves and three compares.
+template <int X, int UP>
+PSG_DEV void sort_step1(int64_t& c, int lane) {
+  const int64_t pc = (int64_t)xchg64<X>((uint64_t)c);
+  const bool take = (pc < c) != ((lane & UP) != 0);
+  c = take ? pc : c;
+}
+template <int D>
+PSG_DEV void half_clean1(int64_t& c, int lane) {
+  sort_step1<D, D>(c, lane);
+  if constexpr (D > 1) half_clean1<D / 2>(c, lane);
+}
+template <int SIZE = 2>
+PSG_DEV void wave_sort_packed(int64_t& c, int lane) {
+  sort_step1<SIZE - 1, SIZE / 2>(c, lane);
+  if constexpr (SIZE >= 4) half_clean1<SIZE / 4>(c, lane);
+  if constexpr (SIZE < 64) wave_sort_packed<SIZE * 2>(c, lane);
+}
+
 // 64 x 64 bit-matrix transpose across a wave: lane i holds row i; afterwards lane j holds
 // column j (bit i = bit j of row i). The six swap stages of the block transpose: at stage
 // s, the lane pair (i, i ^ s) exchanges the off-diagonal s x s blocks of its 2s x 2s block.
@@ -336,10 +359,19 @@ epsilon_kernel(KArgs a) {
           const int64_t key = total_key(x);
           int32_t spid_r = 0;  // W = 1: pid at sorted position = lane
           if constexpr (W == 1) {
-            int64_t skey = g.valid ? key : INT64_MAX;  // padding lanes sort last
-            spid_r = g.lane;
-            wave_sort_key_pid(skey, spid_r, g.lane);
-            const double xs = __shfl(x, spid_r);
+            // padding lanes sort last: no valid key reaches INT64_MAX's top 58 bits (NaN's is 0x7ff8 << 48)
+            int64_t c = ((g.valid ? key : INT64_MAX) & ~(int64_t)63) | g.lane;
+            wave_sort_packed(c, g.lane);
+            spid_r = (int32_t)(c & 63);
+            double xs = __shfl(x, spid_r);
+            const int64_t ks = total_key(xs);
+            const int64_t kn = (int64_t)__shfl_down((long long)ks, 1);
+            if (g.any(g.lane + 1 < n && kn < ks)) {  // rare: keys within 64 ulp out of pid order
+              int64_t skey = g.valid ? key : INT64_MAX;
+              spid_r = g.lane;
+              wave_sort_key_pid(skey, spid_r, g.lane);
+              xs = __shfl(x, spid_r);
+            }
             if (g.lane < n) sx[g.lane] = xs;
           } else {
             L.keys[g.pid] = key;
