@@ -142,6 +142,10 @@ def pmc_profile(args):
     (profiles/*/pmc_summary.json, scripts/summarize_profile.py): HBM bytes per launch and
     instructions per instance-round, with whether it was taken on this very libpsg.so."""
     import glob
+    try:
+        sha = lib_sha256()
+    except OSError:
+        sha = None
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json"))):
         try:
@@ -152,14 +156,10 @@ def pmc_profile(args):
         if ("otr_kernel<1" in d.get("kernel", "") and "hbm" in d and "per_instance_round" in d
                 and w.get("n") == args.n and w.get("rounds") == args.rounds
                 and w.get("instances_per_gpu") == args.instances and w.get("value_range") == args.V):
-            best = (os.path.relpath(f, ROOT), d)
-    if best is None:
-        return None
-    try:
-        same = best[1].get("lib_sha256") == lib_sha256()
-    except OSError:
-        same = False
-    return best[0], best[1], same
+            # a profile of this very build wins over any other; else the last in name order
+            if best is None or best[2] is False or d.get("lib_sha256") == sha:
+                best = (os.path.relpath(f, ROOT), d, sha is not None and d.get("lib_sha256") == sha)
+    return best
 
 
 def _cpu_quota():

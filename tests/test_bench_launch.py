@@ -95,3 +95,26 @@ def test_parallelism_label_states_whether_rccl_ran():
     assert "x8 ranks" in bench.parallelism_label("ranks", 8, None, 10)
     dl = bench.parallelism_label("device-list", 1, [0, 1], 10)
     assert "RCCL" not in dl and "[0, 1]" in dl
+
+
+def test_pmc_profile_prefers_the_profile_of_this_build(monkeypatch, tmp_path):
+    """A profile taken on the running libpsg.so wins over a later-named one of another build."""
+    a = _args()
+    w = {"n": a.n, "rounds": a.rounds, "instances_per_gpu": a.instances, "value_range": a.V}
+
+    def put(name, sha):
+        d = tmp_path / "profiles" / name
+        d.mkdir(parents=True)
+        (d / "pmc_summary.json").write_text(json.dumps(
+            {"kernel": "psg::otr_kernel<1, false>", "hbm": {}, "per_instance_round": {}, "workload": w,
+             "lib_sha256": sha}))
+
+    put("r6_otr_n64", "this")
+    put("r6m_otr_n64", "older")
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "lib_sha256", lambda: "this")
+    path, _, same = bench.pmc_profile(a)
+    assert path == os.path.join("profiles", "r6_otr_n64", "pmc_summary.json") and same
+    monkeypatch.setattr(bench, "lib_sha256", lambda: "another")
+    path, _, same = bench.pmc_profile(a)
+    assert path == os.path.join("profiles", "r6m_otr_n64", "pmc_summary.json") and not same
