@@ -225,26 +225,66 @@ PSG_DEV void wave_sort_packed(int64_t& c, int lane) {
 }
 
 // 64 x 64 bit-matrix transpose across a wave: lane i holds row i; afterwards lane j holds
-// column j (bit i = bit j of row i). The six swap stages of the block transpose: at stage
-// s, the lane pair (i, i ^ s) exchanges the off-diagonal s x s blocks of its 2s x 2s block.
-// Branch-free: the upper lane of a pair keeps its ~LO blocks and takes the partner's ~LO
-// blocks shifted down into LO, the lower lane the mirror image (two selects and two bitfield
-// inserts instead of a divergent if / else).
-template <int S, uint64_t LO>
-PSG_DEV uint64_t transpose_stage(uint64_t r, int lane) {
-  const uint64_t p = xshfl64<S>(r, lane);
-  const bool up = (lane & S) != 0;
-  const uint64_t keep = up ? ~LO : LO;
-  const uint64_t moved = up ? (p >> S) : (p << S);
-  return (r & keep) | (moved & ~keep);
+// column j (bit i = bit j of row i). Stage S (any order: each swaps one bit of the row index
+// with the same bit of the column index): the lane pair (i, i ^ S) exchanges the off-diagonal
+// S x S blocks of its 2S x 2S block — the lower lane keeps its LO blocks and takes the
+// partner's LO blocks into its ~LO ones, the upper lane the mirror image. On the two 32-bit
+// halves of the row:
+//   S = 32  one v_permlane32_swap (the lower lanes' high words <-> the upper lanes' low words);
+//   S = 16  per word one v_permlane16_swap (own and partner's word land in the two outputs)
+//           and one v_perm_b32 byte select (bytes 0, 1 / 2, 3 of each);
+//   S = 8   per word a ds_bpermute and one v_perm_b32 byte select;
+//   S < 8   per word a ds_bpermute, a rotate (v_alignbit: the wrapped bits fall in the blocks
+//           the lane keeps) and a bit-field select.
+// (round 5: a 64-bit shift / select form of every stage; this one has no 64-bit operations.)
+PSG_DEV void transpose_s32(uint32_t& lo, uint32_t& hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+  lo = (uint32_t)r[0];
+  hi = (uint32_t)r[1];
+}
+PSG_DEV uint32_t transpose_s16(uint32_t w, uint32_t sel) {
+  const auto r = __builtin_amdgcn_permlane16_swap(w, w, false, false);  // even rows: (own, partner); odd: (partner, own)
+  return __builtin_amdgcn_perm((uint32_t)r[1], (uint32_t)r[0], sel);
+}
+template <int S>
+PSG_DEV uint32_t transpose_small(uint32_t w, bool up) {
+  constexpr uint32_t LO = S == 4 ? 0x0F0F0F0Fu : S == 2 ? 0x33333333u : 0x55555555u;
+  const uint32_t p = xshfl<S>(w, 0);
+  const uint32_t moved = __builtin_amdgcn_alignbit(p, p, up ? S : 32 - S);  // rotate right
+  const uint32_t keep = up ? ~LO : LO;
+  return (w & keep) | (moved & ~keep);
 }
 PSG_DEV uint64_t wave_transpose64(uint64_t r, int lane) {
-  r = transpose_stage<32, 0x00000000FFFFFFFFull>(r, lane);
-  r = transpose_stage<16, 0x0000FFFF0000FFFFull>(r, lane);
-  r = transpose_stage<8, 0x00FF00FF00FF00FFull>(r, lane);
-  r = transpose_stage<4, 0x0F0F0F0F0F0F0F0Full>(r, lane);
-  r = transpose_stage<2, 0x3333333333333333ull>(r, lane);
-  return transpose_stage<1, 0x5555555555555555ull>(r, lane);
+  uint32_t lo = (uint32_t)r, hi = (uint32_t)(r >> 32);
+  transpose_s32(lo, hi);
+  {
+    // v_perm_b32(s0 = r[1], s1 = r[0]): bytes 0-3 of r[0] are selectors 0-3, of r[1] 4-7
+    const uint32_t sel = (lane & 16) ? 0x07060302u : 0x05040100u;
+    lo = transpose_s16(lo, sel);
+    hi = transpose_s16(hi, sel);
+  }
+  {
+    // lower: (w.b0, p.b0, w.b2, p.b2); upper: (p.b1, w.b1, p.b3, w.b3); s0 = p, s1 = w
+    const uint32_t sel = (lane & 8) ? 0x03070105u : 0x06020400u;
+    lo = __builtin_amdgcn_perm(xshfl<8>(lo, lane), lo, sel);
+    hi = __builtin_amdgcn_perm(xshfl<8>(hi, lane), hi, sel);
+  }
+  {
+    const bool up = (lane & 4) != 0;
+    lo = transpose_small<4>(lo, up);
+    hi = transpose_small<4>(hi, up);
+  }
+  {
+    const bool up = (lane & 2) != 0;
+    lo = transpose_small<2>(lo, up);
+    hi = transpose_small<2>(hi, up);
+  }
+  {
+    const bool up = (lane & 1) != 0;
+    lo = transpose_small<1>(lo, up);
+    hi = transpose_small<1>(hi, up);
+  }
+  return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
 // Slots: 0 EpsAgreement (no NaN decision, max - min <= eps), 1 EpsValidity (every
