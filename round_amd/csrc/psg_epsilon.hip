@@ -247,9 +247,9 @@ PSG_DEV uint32_t transpose_s16(uint32_t w, uint32_t sel) {
   return __builtin_amdgcn_perm((uint32_t)r[1], (uint32_t)r[0], sel);
 }
 template <int S>
-PSG_DEV uint32_t transpose_small(uint32_t w, bool up) {
+PSG_DEV uint32_t transpose_small(uint32_t w, bool up, int lane) {
   constexpr uint32_t LO = S == 4 ? 0x0F0F0F0Fu : S == 2 ? 0x33333333u : 0x55555555u;
-  const uint32_t p = xshfl<S>(w, 0);
+  const uint32_t p = xshfl<S>(w, lane);
   const uint32_t moved = __builtin_amdgcn_alignbit(p, p, up ? S : 32 - S);  // rotate right
   const uint32_t keep = up ? ~LO : LO;
   return (w & keep) | (moved & ~keep);
@@ -271,18 +271,18 @@ PSG_DEV uint64_t wave_transpose64(uint64_t r, int lane) {
   }
   {
     const bool up = (lane & 4) != 0;
-    lo = transpose_small<4>(lo, up);
-    hi = transpose_small<4>(hi, up);
+    lo = transpose_small<4>(lo, up, lane);
+    hi = transpose_small<4>(hi, up, lane);
   }
   {
     const bool up = (lane & 2) != 0;
-    lo = transpose_small<2>(lo, up);
-    hi = transpose_small<2>(hi, up);
+    lo = transpose_small<2>(lo, up, lane);
+    hi = transpose_small<2>(hi, up, lane);
   }
   {
     const bool up = (lane & 1) != 0;
-    lo = transpose_small<1>(lo, up);
-    hi = transpose_small<1>(hi, up);
+    lo = transpose_small<1>(lo, up, lane);
+    hi = transpose_small<1>(hi, up, lane);
   }
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
