@@ -604,7 +604,7 @@ PSG_DEV void kset_tail(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst
   Checks ck;
   ck.ffv = (int32_t)(m & 0xFFu);
   uint32_t fw = ((uint32_t)m >> 8) & 0xF0Fu;  // decider bit j, not-initial bit 8 + j
-  int32_t decision[W], halt_round[W], mainx[W];
+  int32_t decision[W], halt_round[W];
   uint32_t al[W];
 #pragma unroll
   for (int j = 0; j < W; ++j) {
@@ -612,9 +612,6 @@ PSG_DEV void kset_tail(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst
     halt_round[j] = b == 0xFFu ? -1 : (int32_t)b;
     decision[j] = 0;
     if (P.val[j] && halt_round[j] >= 0) decision[j] = a.hand_dec[i * (uint64_t)n + (uint64_t)P.pid(j)];
-    // final x = pick(t): a process halted before the hand-off decided pick of its own (frozen) t,
-    // every other process holds the common t
-    mainx[j] = halt_round[j] >= 0 ? decision[j] : pu;
     al[j] = P.val[j] & (halt_round[j] >= 0 ? 0u : 1u);
   }
   Mask<W> act = P.ballot(al);
@@ -730,6 +727,12 @@ PSG_DEV void kset_tail(const Pk<W>& P, const KArgs& a, uint64_t i, uint64_t inst
     check(k + 1);
     pt.mark(live ? 4 : 5);
   }
+  // final x = pick(t): a process halted before the hand-off (halt round < k0) decided pick of its
+  // own (frozen) t, every other process holds the common t (formed here, not kept live across the
+  // rounds: 4 VGPRs)
+  int32_t mainx[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) mainx[j] = (halt_round[j] >= 0 && halt_round[j] < k0) ? decision[j] : pu;
   pk_finish<W>(P, a, i, ck, 2, decision, halt_round, halt_round, mainx, bc);
   pt.mark(3);
 }
