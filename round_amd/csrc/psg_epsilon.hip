@@ -404,9 +404,11 @@ epsilon_kernel(KArgs a) {
             wave_sort_packed(c, g.lane);
             spid_r = (int32_t)(c & 63);
             double xs = __shfl(x, spid_r);
+            // position t's full key against position t - 1's (DPP wave_shr:1, no LDS round trip)
             const int64_t ks = total_key(xs);
-            const int64_t kn = (int64_t)__shfl_down((long long)ks, 1);
-            if (g.any(g.lane + 1 < n && kn < ks)) {  // rare: keys within 64 ulp out of pid order
+            const int64_t kp = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)ks, 0x138, 0xF, 0xF, false) |
+                                         ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(ks >> 32), 0x138, 0xF, 0xF, false) << 32));
+            if (g.any(g.lane >= 1 && g.lane < n && kp > ks)) {  // rare: keys within 64 ulp out of pid order
               int64_t skey = g.valid ? key : INT64_MAX;
               spid_r = g.lane;
               wave_sort_key_pid(skey, spid_r, g.lane);

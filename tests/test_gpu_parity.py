@@ -382,3 +382,29 @@ def test_gpu_epsilon_host_inputs(n, f, dup, oracle_mod):
         res = gr.run(5, count, per_instance=True)
         dec, dround = gr.decisions()
     _check_eps(gr, res, dec, dround, 5, count, init=init, oracle_mod=oracle_mod)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,f", [(64, 5), (40, 4)])
+def test_gpu_epsilon_keys_within_64_ulp_against_pid_order(n, f, oracle_mod):
+    """Initial values a few ulp apart, descending by pid: the one-word sort (top 58 key bits,
+    ties by pid) leaves them against their (key, pid) order, so its adjacent-key test must send
+    every such round to the (key, pid) network (psg_epsilon.hip). Later rounds' means are
+    also within a few ulp of each other."""
+    import random
+    import struct
+    rng = random.Random(31 + n)
+    count = 200
+
+    def ulps(x, k):
+        return struct.unpack("<d", struct.pack("<q", struct.unpack("<q", struct.pack("<d", x))[0] + k))[0]
+
+    init = []
+    for i in range(count):
+        base = rng.uniform(0.1, 4.0) * (-1 if i % 3 == 0 else 1)
+        init.append([ulps(base, (n - p) * (1 + i % 3)) for p in range(n)])
+    with psync.GpuRound(psync.EpsilonConsensus(f, 1e-15), n, seed=71, batch_capacity=count) as gr:
+        gr.load_inputs(0, count, init)
+        res = gr.run(0, count, per_instance=True)
+        dec, dround = gr.decisions()
+    _check_eps(gr, res, dec, dround, 0, count, init=init, oracle_mod=oracle_mod)
