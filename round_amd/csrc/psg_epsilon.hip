@@ -354,7 +354,12 @@ epsilon_kernel(KArgs a) {
     double x0 = 0.0;
     if (g.valid) {
       if (a.init_f64) {
-        x0 = a.init_f64[init_row(a, i, inst) * (uint64_t)n + g.pid];
+        // pid through an opaque copy: the lane's element pointer is formed here, once per
+        // instance, instead of hoisted out of the instance loop (a 64-bit VGPR pair spilled to
+        // scratch at 6 waves/SIMD)
+        int pid = g.pid;
+        asm volatile("" : "+v"(pid));
+        x0 = a.init_f64[init_row(a, i, inst) * (uint64_t)n + (uint64_t)pid];
       } else {  // uniform [0,1) with 53 bits (Random.nextDouble shape, Epsilon.scala:94)
         const uint64_t w = rword(a.seed, inst, ROUND_INIT, (uint32_t)g.pid, 0);
         x0 = (double)(w >> 11) * 0x1.0p-53;
@@ -390,7 +395,9 @@ epsilon_kernel(KArgs a) {
         // per lane: min, max, V(2f) and the trimmed every-2f-th sum over the members of
         // its own V (Epsilon.scala:31-42); no V is read in a round where every process that
         // still runs decides (r > maxR), so that round skips the sort
-        double first = 0.0, last = 0.0, e2f = 0.0, sum = 0.0;
+        // round 0: span = max - min of V and acc = V(2f); later rounds: acc = the trimmed sum
+        // (one pair of doubles for both: they are never live together)
+        double span = 0.0, acc = 0.0;
         int cnt = 0;
         if (g.any(!halted && k <= maxR)) {
           // sort every process's current x in total order (ties by pid): W = 1 a wave bitonic
@@ -443,12 +450,11 @@ epsilon_kernel(KArgs a) {
             if (!halted && m > 0) {
               const RankSel rs(Us);
               if (k == 0) {
-                first = sx[__builtin_ctzll(Us)];
-                last = sx[63 - __builtin_clzll(Us)];
-                if (m > 2 * f) e2f = sx[rs.at((uint32_t)(2 * f), L.sel8)];
+                span = sx[63 - __builtin_clzll(Us)] - sx[__builtin_ctzll(Us)];
+                if (m > 2 * f) acc = sx[rs.at((uint32_t)(2 * f), L.sel8)];
               } else if (k <= maxR) {
                 for (int j = f; j < m - f; j += 2 * f) {  // ascending left fold from 0.0
-                  sum += sx[rs.at((uint32_t)j, L.sel8)];
+                  acc += sx[rs.at((uint32_t)j, L.sel8)];
                   ++cnt;
                 }
               }
@@ -456,6 +462,7 @@ epsilon_kernel(KArgs a) {
           } else {
             // W > 1: every lane walks the sorted list once with broadcast LDS reads;
             // the selected members are tracked with a running index (no modulo)
+            double first = 0.0, last = 0.0, e2f = 0.0, sum = 0.0;
             int j = 0, nsel = f;
             const int jhi = m - f;
             for (int t = 0; t < n; ++t) {
@@ -472,19 +479,21 @@ epsilon_kernel(KArgs a) {
                 ++j;
               }
             }
+            span = last - first;
+            acc = k == 0 ? e2f : sum;
           }
         }
         if (!halted) {
           H = mor(H, mand(M, Fl));  // halted ++ mailbox.filter(_._2._2)
           if (k == 0) {
             if (m > 0) {  // (empty V: Scala throws; left unchanged)
-              const double r1 = log_ocml((last - first) / eps) / logc;
+              const double r1 = log_ocml(span / eps) / logc;
               maxR = d2i(ceil(r1));
               if (a.variant == 1) maxR = 0;  // variant 1: mutation, no approximation rounds
-              if (m > 4 * f) x = e2f;  // reduce(2f, V).head
+              if (m > 4 * f) x = acc;  // reduce(2f, V).head
             }
           } else if (k <= maxR) {
-            x = sum / (double)cnt;  // sel.sum / sel.size (NaN for an empty sel)
+            x = acc / (double)cnt;  // sel.sum / sel.size (NaN for an empty sel)
           } else {
             decided = true;  // callback.decide(x); exitAtEndOfRound
             decision = x;
