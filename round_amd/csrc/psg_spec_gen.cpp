@@ -1342,9 +1342,13 @@ std::string module_source(ParsedSpec& P, const Compiled& prog, int alg, bool fus
     std::vector<int> waves;
     if (n > 0) waves.push_back((n + 63) / 64);
     else waves = {1, 2, 3, 4};
-    // the compiler's mul_lo / mul_hi Philox products: the inline v_mad_u64_u32 form that wins in the
-    // library's round kernels measured 4-6 % slower in the fused modules (round-4 A/B)
-    src = "#define PSG_FUSED_MODULE 1\n#ifndef PSG_PHILOX_MAD64\n#define PSG_PHILOX_MAD64 0\n#endif\n" + src + fused_source(alg, waves);
+    // Philox products: the inline v_mad_u64_u32 form (carry in VCC, the library's round kernels'
+    // choice) for OTR / OTR2 — round 6, at 6 waves/SIMD: fused OTR 36.50 -> 35.21 ms; LastVoting
+    // neutral (81.46 / 81.55) — and the compiler's mul_lo / mul_hi pair for the others (round 4:
+    // the inline form 4-6 % slower there)
+    const int mad64 = alg == PSG_ALG_OTR || alg == PSG_ALG_OTR2 ? 2 : 0;
+    src = "#define PSG_FUSED_MODULE 1\n#ifndef PSG_PHILOX_MAD64\n#define PSG_PHILOX_MAD64 " + S(mad64) + "\n#endif\n" + src +
+          fused_source(alg, waves);
   }
   return src;
 }
