@@ -335,7 +335,8 @@ int psg_spec_compile_native(const char* text, int32_t alg, int32_t fused, int32_
  * already guarded by their round invariants, (phase 1) — so the rewrites can be checked
  * against the Spec as written under any evaluator (tests). Same buffer contract as
  * psg_spec_native_source. Generator options for all three entry points (comma-separated:
- * nosym, nosplit, D<NAME>=<VALUE>) come from psg_spec_set_options on the calling thread, else
+ * nosym, sym — the symmetric-check-point lowering off / on; fused LastVoting modules default to
+ * off —, nosplit, nofrozen, D<NAME>=<VALUE>) come from psg_spec_set_options on the calling thread, else
  * from the environment variable PSG_SPEC_OPTIONS; an unknown option, a define outside the
  * generator knobs (PSG_PHASE_TIMERS, the PSG_*_WPE occupancy targets and the exact-alternative
  * switches PSG_PHILOX_OPAQUE_KEYS, PSG_PHILOX_MAD64, PSG_XSHFL_MASK, PSG_QUEUE_CHUNK[_WIDE],

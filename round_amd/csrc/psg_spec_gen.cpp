@@ -36,13 +36,15 @@ namespace {
 bool is_var(const Tree& T, int e, int uid) { return T.nodes[e].k == VAR && T.nodes[e].uid == uid; }
 
 // Generator options (experiments and profiling builds), comma-separated: "nosym" (no
-// symmetric-check-point lowering), "nosplit" (no split foralls / hoisted conjuncts),
+// symmetric-check-point lowering), "sym" (that lowering also where it is off by default: fused
+// LastVoting modules), "nosplit" (no split foralls / hoisted conjuncts),
 // "D<NAME>=<VALUE>" (a #define at the top of the module, e.g. DPSG_PHASE_TIMERS=1). They change
 // the source, hence the cache key. Per thread: psg_spec_set_options sets the calling thread's
 // string, otherwise the environment variable PSG_SPEC_OPTIONS is read; every entry point parses
 // them into its own thread's GenOptions, so concurrent callers (JVM threads) never share state.
 struct GenOptions {
   bool symmetric = true, split = true, frozen = true;
+  bool sym_explicit = false;  // "sym" / "nosym" given: no per-algorithm default
   std::vector<std::string> defines;
 };
 thread_local GenOptions g_opts;        // this thread's options for the generation in progress
@@ -55,7 +57,10 @@ GenOptions parse_options(const std::string& t) {
   while (i <= t.size()) {
     const size_t j = t.find(',', i);
     const std::string tok = t.substr(i, j == std::string::npos ? std::string::npos : j - i);
-    if (tok == "nosym") o.symmetric = false;
+    if (tok == "nosym" || tok == "sym") {
+      o.symmetric = tok == "sym";
+      o.sym_explicit = true;
+    }
     else if (tok == "nosplit") o.split = false;
     else if (tok == "nofrozen") o.frozen = false;
     else if (tok.size() > 1 && tok[0] == 'D') {
@@ -1331,7 +1336,13 @@ std::string env_or(const char* name, const std::string& dflt) {
 
 // The full module source of compile_native(text, alg, fused, n) and its cache key.
 std::string module_source(ParsedSpec& P, const Compiled& prog, int alg, bool fused, int n) {
+  // fused LastVoting: no symmetric-check-point lowering unless asked for ("sym") — its check points
+  // are rarely symmetric, and without the second lowering the module measured 2 % faster (round 6,
+  // 81.55 -> 79.90 ms at 8 waves/SIMD, scripts/probe_fused.py)
+  const bool sym_saved = g_opts.symmetric;
+  if (fused && alg == PSG_ALG_LAST_VOTING && !g_opts.sym_explicit) g_opts.symmetric = false;
   std::string src = codegen_hip(P, prog, alg);
+  g_opts.symmetric = sym_saved;
   std::string defs;
   for (const std::string& d : g_opts.defines) {
     const size_t eq = d.find('=');

@@ -228,3 +228,16 @@ def test_module_toolchain_independent_of_torch(tmp_path):
         out[mode] = r.stdout.split()
     assert out["plain"][:2] == out["torch"][:2]  # same cache key, same code object bytes
     assert any(p.startswith("/opt/rocm") for p in out["torch"][2].split("|")), out["torch"]
+
+
+def test_fused_lastvoting_defaults_to_no_symmetric_lowering():
+    """Fused LastVoting modules drop the symmetric-check-point lowering by default (measured faster,
+    psg_spec_gen.cpp module_source); "sym" brings it back, "nosym" is the default's own source; the
+    non-fused LastVoting module and fused OTR keep it."""
+    t = F.to_text(F.lv_spec())
+    fused = lib.spec_native_source(t, abi.PSG_ALG_LAST_VOTING, fused=True, n=64)
+    assert "spec::uniform<" not in fused
+    assert fused == lib.spec_native_source(t, abi.PSG_ALG_LAST_VOTING, fused=True, n=64, options=["nosym"])
+    assert "spec::uniform<" in lib.spec_native_source(t, abi.PSG_ALG_LAST_VOTING, fused=True, n=64, options=["sym"])
+    assert "spec::uniform<" in lib.spec_native_source(t, abi.PSG_ALG_LAST_VOTING)
+    assert "spec::uniform<" in lib.spec_native_source(F.to_text(F.otr_spec()), abi.PSG_ALG_OTR, fused=True, n=64)
