@@ -339,7 +339,7 @@ int psg_spec_compile_native(const char* text, int32_t alg, int32_t fused, int32_
  * off —, nosplit, nofrozen, D<NAME>=<VALUE>) come from psg_spec_set_options on the calling thread, else
  * from the environment variable PSG_SPEC_OPTIONS; an unknown option, a define outside the
  * generator knobs (PSG_PHASE_TIMERS, the PSG_*_WPE occupancy targets and the exact-alternative
- * switches PSG_PHILOX_OPAQUE_KEYS, PSG_PHILOX_MAD64, PSG_XSHFL_MASK, PSG_QUEUE_CHUNK[_WIDE],
+ * switches PSG_PHILOX_OPAQUE_KEYS, PSG_PHILOX_MAD64, PSG_XSHFL_MASK, PSG_QUEUE_CHUNK[_WIDE|_LANE],
  * PSG_MAJ_BITVOTE, PSG_BO_FLAGS_DPP) or a non-integer value makes the entry point return
  * PSG_EINVAL. */
 int psg_spec_rewrite_text(const char* text, int32_t alg, char* out, size_t* out_len, char* err, size_t err_len);

@@ -826,12 +826,17 @@ PSG_DEV void lds_sync() {
 #define PSG_QUEUE_CHUNK_WIDE 4  // W > 1 (one instance per block): 1 -> 4 measured +2-4 % on C4/C5
 #endif
 #ifndef PSG_QUEUE_CHUNK
-#define PSG_QUEUE_CHUNK 8  // W = 1: 4 -> 8 measured headline 19.24 -> 19.08 ms, C3 46.88 -> 46.78 (round 6)
+#define PSG_QUEUE_CHUNK 4
 #endif
-template <int W, int REGION = 0>
+// OTR / OTR2, LastVoting, ShortLastVoting at W = 1 (CHUNK argument): 4 -> 8 measured headline
+// 19.24 -> 19.08 ms, C3 46.88 -> 46.78 (round 6); the packed kernels and Epsilon lost 1-4 % at 8
+#ifndef PSG_QUEUE_CHUNK_LANE
+#define PSG_QUEUE_CHUNK_LANE 8
+#endif
+template <int W, int REGION = 0, int CHUNK = 0>
 struct InstanceQueue {
   static_assert(REGION >= 0 && REGION < NQUEUE_REGIONS, "queue region");
-  static constexpr uint64_t kChunk = W == 1 ? PSG_QUEUE_CHUNK : PSG_QUEUE_CHUNK_WIDE;
+  static constexpr uint64_t kChunk = CHUNK > 0 ? CHUNK : (W == 1 ? PSG_QUEUE_CHUNK : PSG_QUEUE_CHUNK_WIDE);
   static constexpr uint64_t kDone = ~0ull;
   uint64_t cur = 0, lim = 0;  // uniform: [cur, lim) is this group's current chunk
   int tries = 0;              // queues drained so far

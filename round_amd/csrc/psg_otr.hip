@@ -132,7 +132,7 @@ PSG_DEV void otr_body(const KArgs& a) {
 
   PhaseTimers pt;  // profiling builds only: t0 setup, t1 active round, t2 frozen round, t3 finish
   pt.start();
-  InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
+  InstanceQueue<W, 0, W == 1 ? PSG_QUEUE_CHUNK_LANE : 0> Q;  // dynamic instance distribution (psg_device.hpp)
   StepTally tally;     // per-lane process-round steps, reduced once per wave
   // Host-supplied initial values are loaded one instance ahead: the next row's load is
   // issued when an instance starts and consumed when the next one does, so its latency

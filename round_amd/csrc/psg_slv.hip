@@ -77,7 +77,7 @@ PSG_DEV void slv_body(const KArgs& a) {
   const Mask<W> full = mfull<W>(n);
   const uint32_t myh = scala_improve((uint32_t)g.pid);
 
-  InstanceQueue<W> Q;  // dynamic instance distribution (psg_device.hpp)
+  InstanceQueue<W, 0, W == 1 ? PSG_QUEUE_CHUNK_LANE : 0> Q;  // dynamic instance distribution (psg_device.hpp)
   for (uint64_t i = Q.take(a); i != Q.kDone; i = Q.take(a)) {
     const uint64_t inst = a.ids ? a.ids[i] : a.inst_begin + i;
     Sched<W, XHO> sc;

@@ -81,7 +81,7 @@ GenOptions parse_options(const std::string& t) {
       // else (PSG_MAX_CHECKS, PSG_FUSED_MODULE, probe switches) would change what a product
       // module computes
       static const char* const kKnobs[] = {"PSG_PHASE_TIMERS", "PSG_PHILOX_OPAQUE_KEYS", "PSG_PHILOX_MAD64",
-                                           "PSG_XSHFL_MASK",   "PSG_QUEUE_CHUNK",        "PSG_QUEUE_CHUNK_WIDE",
+                                           "PSG_XSHFL_MASK",   "PSG_QUEUE_CHUNK",        "PSG_QUEUE_CHUNK_WIDE",   "PSG_QUEUE_CHUNK_LANE",
                                            "PSG_MAJ_BITVOTE",  "PSG_BO_FLAGS_DPP"};
       bool ok = name.size() > 8 && name.compare(0, 4, "PSG_") == 0 && name.compare(name.size() - 4, 4, "_WPE") == 0;
       for (const char* k : kKnobs) ok = ok || name == k;
